@@ -1,0 +1,202 @@
+/* pycatkin_amd C-ABI: batched mean-field microkinetic (MK) solves on MI355X.
+ *
+ * One "condition" = one independent MK model instance (a temperature /
+ * pressure / descriptor-grid point).  Every per-condition array is
+ * structure-of-arrays, device-resident, fp64: element (k, c) of an array with
+ * leading dimension ld and condition stride s lives at ptr[k*ld + c*s]; a
+ * stride of 0 broadcasts one column to every condition.
+ *
+ * The network is compiled host-side (pycatkin_amd/network.py) into two flat
+ * blobs -- int32 `ip` and float64 `dp` -- whose layout is given by the
+ * PCK_I_* / PCK_D_* header slots below, and uploaded once with
+ * pck_network_create().
+ *
+ * Each entry point replaces one reference (PyCatKin) Python routine that a
+ * ctypes / FFI binding would call for the whole batch:
+ *
+ *   pck_rate_constants  <- Reaction.calc_rate_constants      pycatkin/classes/reaction.py:94
+ *                          (+ State.calc_free_energy          pycatkin/classes/state.py:556,
+ *                             ScalingState.calc_free_energy   state.py:708,
+ *                             UserDefinedReaction.calc_reaction_energy reaction.py:222)
+ *   pck_species_rates   <- System.species_odes + Reactor.rhs  pycatkin/classes/old_system.py:227,
+ *                                                             pycatkin/classes/reactor.py:91,141
+ *                          System.get_dydt / _fun_ss          pycatkin/classes/system.py:396,528
+ *   pck_jacobian        <- System.species_jacobian + Reactor.jacobian old_system.py:293, reactor.py:103,161
+ *                          System.get_jacobian / _jac_ss      system.py:493,547
+ *   pck_solve           <- System.solve_odes (+ find_steady)  old_system.py:315 (385)
+ *                          SteadyStateSolver.solve_ode        pycatkin/classes/solver.py:374
+ *                          System.run_and_return_tof / activity old_system.py:470,517
+ *   pck_drc             <- System.degree_of_rate_control      old_system.py:490
+ *
+ * All functions return 0 on success and a negative PCK_E_* code on failure;
+ * pck_last_error() returns a message for the calling thread.  Device pointers
+ * only; `stream` is a hipStream_t (NULL = default stream).  Launches are
+ * asynchronous on `stream` unless noted.
+ */
+#ifndef PYCATKIN_AMD_H
+#define PYCATKIN_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PCK_ABI_VERSION 1
+
+/* error codes */
+#define PCK_OK 0
+#define PCK_E_ARG (-1)      /* bad argument / blob layout */
+#define PCK_E_HIP (-2)      /* HIP runtime error */
+#define PCK_E_SIZE (-3)     /* network exceeds the compiled kernel limits */
+
+/* kernel limits (thread-per-condition solver, dense state in registers) */
+#define PCK_MAX_DYN 8       /* dynamic species per condition (solver kernels) */
+#define PCK_MAX_DYN_PLAN 64 /* dynamic species a plan may hold (rate constants / energies) */
+#define PCK_MAX_RXN 64      /* active reactions */
+#define PCK_MAX_CONS 4      /* conservation laws */
+#define PCK_MAX_TOF 16      /* TOF terms */
+
+/* int32 blob header slots (ip[0..PCK_I_HDR)) */
+enum {
+    PCK_I_VERSION = 0, /* == PCK_ABI_VERSION */
+    PCK_I_NDESC,       /* D: descriptors per condition */
+    PCK_I_NTH,         /* thermo states (vib/tran/rot features) */
+    PCK_I_NREG,        /* energy-program registers */
+    PCK_I_NRXN,        /* active reactions R */
+    PCK_I_NDYN,        /* dynamic species NS */
+    PCK_I_NFIX,        /* fixed (non-dynamic) species F */
+    PCK_I_NCONS,       /* conservation laws m */
+    PCK_I_NTOF,        /* TOF terms */
+    PCK_I_OFF_TH,      /* -> th: NTH x {kind, freq_off, freq_cnt, rot_shape} */
+    PCK_I_OFF_REG,     /* -> reg_ptr[NREG+1], reg_clamp[NREG], reg_feat[nnz] */
+    PCK_I_OFF_RX,      /* -> rx: NRXN x {type, reversible, reg_ga, reg_grxn, reg_erxn, arr_if_barrier} */
+    PCK_I_OFF_EXPF,    /* -> forward exponents  [NRXN][NDYN] */
+    PCK_I_OFF_EXPR,    /* -> reverse exponents  [NRXN][NDYN] */
+    PCK_I_OFF_FOLDF,   /* -> forward fixed-species exponents [NRXN][NFIX] */
+    PCK_I_OFF_FOLDR,   /* -> reverse fixed-species exponents [NRXN][NFIX] */
+    PCK_I_OFF_CPIV,    /* -> pivot row of each conservation law [NCONS] */
+    PCK_I_OFF_TOF,     /* -> active-reaction index of each TOF term [NTOF] */
+    PCK_I_HDR
+};
+
+/* float64 blob header-less layout: offsets are stored in the int blob */
+enum {
+    PCK_D_OFF_SLOT0 = PCK_I_HDR, /* ip[PCK_D_OFF_SLOT0 + k] = dp offset of block k: */
+    PCK_D_TH = 0,    /* th: NTH x {zpe [eV], mass [amu], sigma, rotI = sqrt(prod nonzero I) [kg m^2], Gvibr given (NaN = compute)} */
+    PCK_D_FREQ,      /* frequency table (Hz) */
+    PCK_D_REGCOEF,   /* reg_coef[nnz] */
+    PCK_D_RX,        /* rx: NRXN x {kads_c, kdes_c, kdes_texp} */
+    PCK_D_STOICH,    /* S[NDYN][NRXN] (weights incl. scaling / site density) */
+    PCK_D_DYN,       /* dyn: NDYN x {conc_factor, rowscale0, rowscale_T, flow_rate} */
+    PCK_D_CONS,      /* C[NCONS][NDYN] */
+    PCK_D_NBLK
+};
+#define PCK_IP_MIN (PCK_I_HDR + PCK_D_NBLK)
+
+/* register feature index space: 0 = constant 1, 1 = T, 2 .. 2+D-1 = descriptors,
+ * then 3 per thermo state (vib, tran, rot), then earlier registers. */
+
+/* reaction rate-constant types (reaction.py:94-168) */
+enum {
+    PCK_RX_ARRHENIUS = 0,  /* kf = kBT/h exp(-max(dGa,0)/RT); kr = kf/exp(-dGrxn/RT) */
+    PCK_RX_ADS_KEQ = 1,    /* kf = kads;  kr = kads/exp(-dGrxn/RT) (classic) */
+    PCK_RX_DES_KEQ = 2,    /* kr = kads;  kf = kads*exp(-dGrxn/RT) (classic) */
+    PCK_RX_ADS_KDES = 3,   /* kf = kads;  kr = kdes(-dErxn) (reaction.py:135-147) */
+    PCK_RX_DES_KDES = 4    /* kf = kdes(dErxn); kr = kads (reaction.py:150-162) */
+};
+
+/* thermo state kinds (bit flags) */
+#define PCK_TH_VIB 1
+#define PCK_TH_GAS 2
+
+typedef struct pck_network pck_network;
+
+/* Per-condition inputs (device pointers; see stride rule above). */
+typedef struct {
+    int64_t n;                       /* number of conditions */
+    const double* T;  int64_t sT;    /* temperature [K] */
+    const double* p;  int64_t sp;    /* pressure [Pa] (free energies only) */
+    const double* desc; int64_t ld_desc, s_desc;   /* [D][..] descriptor values (eV) */
+    const double* fixc; int64_t ld_fix, s_fix;     /* [F][..] fixed-species concentrations */
+    const double* y0; int64_t ld_y0, s_y0;         /* [NS][..] initial dynamic state */
+    const double* inflow; int64_t ld_in, s_in;     /* [NS][..] inflow (CSTR gas rows) */
+} pck_conditions;
+
+typedef struct {
+    double t0, t_end;      /* integrate from t0 to t_end */
+    double rtol, atol;     /* local error control (RMS norm) */
+    int32_t max_steps;     /* per condition */
+    int32_t newton;        /* 1: polish to f(y)=0 after the transient (find_steady) */
+    int32_t newton_iters;  /* max Newton iterations */
+    int32_t want_activity; /* 1: write activity (eV) instead of TOF into tof_out */
+    double drc_eps;        /* pck_drc only: relative k perturbation */
+} pck_solve_params;
+
+/* Outputs of pck_solve (device pointers; any may be NULL). */
+typedef struct {
+    double* y; int64_t ld_y;   /* [NS][ld_y] final dynamic state */
+    double* tof;               /* [n] TOF (1/s) or activity (eV) */
+    int32_t* status;           /* [n] PCK_ST_* */
+    int32_t* nsteps;           /* [n] accepted + rejected steps */
+    double* kf; double* kr;    /* [NRXN][ld_k] optional rate-constant dump */
+    int64_t ld_k;
+} pck_outputs;
+
+/* per-condition status codes */
+#define PCK_ST_OK 0
+#define PCK_ST_MAXSTEPS 1
+#define PCK_ST_STEPFAIL 2
+#define PCK_ST_NONFINITE 3
+#define PCK_ST_NEWTON 4
+
+int pck_abi_version(void);
+const char* pck_last_error(void);
+
+/* Upload a compiled network (host blobs) to the current device. */
+int pck_network_create(const int32_t* ip, int64_t n_ip, const double* dp, int64_t n_dp,
+                       pck_network** out);
+int pck_network_destroy(pck_network* net);
+/* Sizes of a created network: dims[0..8] = D, NTH, NREG, NRXN, NDYN, NFIX, NCONS, NTOF, (reserved) */
+int pck_network_dims(const pck_network* net, int32_t* dims);
+
+/* Energy-program registers (eV) per condition: out[r][ld_out], r < NREG.
+ * Replaces State.get_free_energy (state.py:577) / Reaction.get_reaction_energy
+ * (reaction.py:171) / get_reaction_barriers (reaction.py:182) for a batch.
+ * Networks with NDYN == 0 are accepted for this call and pck_rate_constants. */
+int pck_energies(const pck_network* net, const pck_conditions* cond, double* out, int64_t ld_out,
+                 void* stream);
+
+/* kf, kr: [NRXN][ld_k] outputs (1/s or 1/(s Pa^n) as the reference's). */
+int pck_rate_constants(const pck_network* net, const pck_conditions* cond,
+                       double* kf, double* kr, int64_t ld_k, void* stream);
+
+/* Effective rates of the dynamic species at states y ([NS][ld_y]):
+ * dydt[NS][ld_y] = rowscale * (S . net_rates) + flow.  kf/kr as produced by
+ * pck_rate_constants (fixed species are folded in here). */
+int pck_species_rates(const pck_network* net, const pck_conditions* cond,
+                      const double* kf, const double* kr, int64_t ld_k,
+                      const double* y, int64_t ld_y, double* dydt, void* stream);
+
+/* Jacobian d(dydt)/dy: jac[(i*NS + k)][ld_y] (row-major per condition). */
+int pck_jacobian(const pck_network* net, const pck_conditions* cond,
+                 const double* kf, const double* kr, int64_t ld_k,
+                 const double* y, int64_t ld_y, double* jac, void* stream);
+
+/* Fused: rate constants -> stiff integration t0..t_end (L-stable Rosenbrock
+ * W-method) -> optional Newton steady-state polish -> TOF / activity. */
+int pck_solve(const pck_network* net, const pck_conditions* cond,
+              const pck_solve_params* prm, const pck_outputs* out, void* stream);
+
+/* Degree of rate control for every active reaction (old_system.py:490):
+ * xi[j][ld_xi] = (TOF(k_j*(1+eps)) - TOF(k_j*(1-eps))) / (2 eps TOF0).
+ * tof0 (optional) receives the unperturbed TOF; status as pck_solve. */
+int pck_drc(const pck_network* net, const pck_conditions* cond,
+            const pck_solve_params* prm, double* xi, int64_t ld_xi,
+            double* tof0, int32_t* status, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PYCATKIN_AMD_H */

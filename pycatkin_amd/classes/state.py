@@ -1,0 +1,265 @@
+"""State / ScalingState with the reference's constructor and methods
+(pycatkin/classes/state.py).  Free energies are produced as LinearForms over
+device-evaluated thermal features (see pycatkin_amd/energy.py); the numeric
+getters evaluate those forms through the device kernel for one condition.
+"""
+from __future__ import annotations
+
+import copy
+import os
+
+import numpy as np
+
+from ..constants.physical_constants import JtoeV, h
+from ..energy import LinearForm, as_form, feature_form
+
+
+class State:
+    """Mirror of pycatkin.classes.state.State (state.py:8-265)."""
+
+    def __init__(self, state_type=None, name=None, path=None, vibs_path=None, sigma=None,
+                 mass=None, inertia=None, gasdata=None, add_to_energy=None, path_to_pickle=None,
+                 read_from_alternate=None, truncate_freq=True, energy_source=None, freq_source=None,
+                 freq=None, i_freq=None, Gelec=None, Gzpe=None, Gvibr=None, Gtran=None, Grota=None, Gfree=None):
+        if path_to_pickle:
+            raise NotImplementedError('pickled states are not loaded (no unpickling of external files)')
+        if name is None:
+            name = os.path.basename(path)
+        self.state_type = state_type
+        self.name = name
+        self.path = path
+        self.vibs_path = vibs_path
+        self.sigma = sigma
+        self.mass = mass
+        self.inertia = inertia
+        self.gasdata = gasdata
+        self.add_to_energy = add_to_energy
+        self.read_from_alternate = read_from_alternate
+        self.truncate_freq = truncate_freq
+        self.energy_source = energy_source
+        self.freq_source = freq_source
+        self.Gelec = Gelec
+        self.Gzpe = Gzpe
+        self.Gtran = Gtran
+        self.Gvibr = Gvibr
+        self.Grota = Grota
+        self.Gfree = Gfree
+        self.freq = None
+        self.i_freq = None
+        self.shape = None
+        self.atoms = None
+        if freq is not None:                       # state.py:249-253
+            self.freq_source = 'inputfile'
+            self.freq = np.array(sorted(freq, reverse=True), dtype=float)
+            self.i_freq = np.array(sorted(i_freq or [], reverse=True), dtype=float)
+        if self.state_type == 'gas':
+            assert self.sigma is not None
+            if self.inertia is not None:          # state.py:257-264
+                self.inertia = np.array([i if i > 1.0e-12 else 0.0 for i in self.inertia])
+                self.shape = len([i for i in self.inertia if i > 0.0])
+
+    # -- input readers (state.py:266-400) ------------------------------------
+    def get_atoms(self):
+        if isinstance(self.read_from_alternate, dict) and 'get_atoms' in self.read_from_alternate:
+            self.atoms, self.mass, self.inertia = self.read_from_alternate['get_atoms']()
+        if self.atoms is None and (self.mass is None or (self.state_type == 'gas' and self.inertia is None)):
+            from ..functions.outcar import read_outcar
+            self.atoms = read_outcar(self.path)
+            self.mass = self.atoms.total_mass()
+            if self.state_type == 'gas':
+                self.inertia = self.atoms.moments_of_inertia()
+        if self.state_type == 'gas' and self.inertia is not None:
+            self.inertia = np.array([i if i > 1.0e-12 else 0.0 for i in self.inertia])
+            self.shape = len([i for i in self.inertia if i > 0.0])
+
+    def get_vibrations(self, verbose=False):
+        if self.freq_source == 'datafile':
+            with open(self.vibs_path) as fh:
+                lines = fh.readlines()
+            self.freq = np.array([float(l.split('=')[1].split('Hz')[0]) for l in lines if '/' not in l])
+            self.i_freq = np.array([float(l.split('=')[1].split('Hz')[0]) for l in lines if '/' in l])
+            return
+        if self.freq_source == 'inputfile':
+            return
+        freq = i_freq = None
+        if isinstance(self.read_from_alternate, dict) and 'get_vibrations' in self.read_from_alternate:
+            freq, i_freq = copy.deepcopy(self.read_from_alternate['get_vibrations']())
+        if not freq:
+            base = self.vibs_path if self.vibs_path is not None else self.path
+            if base is not None:
+                from ..functions.outcar import read_frequencies
+                freq, i_freq = read_frequencies(base)
+        if freq is not None:
+            freq = list(freq)
+            i_freq = list(i_freq or [])
+            if self.truncate_freq:                # state.py:373-392
+                floor = 12.4 * 1e-3 / (h * JtoeV)
+                freq = [floor if (f * h * JtoeV * 1e3) < 12.4 else f for f in freq]
+                n_dof = len(freq) + len(i_freq) - (3 if self.state_type == 'gas' else 0)
+                if len(freq) < n_dof:
+                    freq += [floor] * (n_dof - len(freq))
+            self.freq = np.array(sorted(freq, reverse=True))
+            self.i_freq = np.array(i_freq)
+        else:
+            self.freq = np.zeros((1, 1))
+            self.i_freq = []
+
+    def calc_electronic_energy(self, verbose=False):
+        """state.py:436-453"""
+        if self.Gelec is None:
+            if self.energy_source == 'datafile':
+                with open(self.path) as fh:
+                    self.Gelec = float(fh.readlines()[0].split('eV')[0])
+            else:
+                if isinstance(self.read_from_alternate, dict) and 'get_electronic_energy' in self.read_from_alternate:
+                    self.Gelec = self.read_from_alternate['get_electronic_energy']()
+                if self.Gelec is None:
+                    from ..functions.outcar import read_outcar
+                    self.Gelec = read_outcar(self.path).energy
+
+    # -- thermo metadata ------------------------------------------------------
+    def _ensure_vib(self):
+        if self.freq is None and self.Gvibr is None:
+            self.get_vibrations()
+
+    def use_freq(self):
+        """Modes kept for ZPE / vibrational free energy (state.py:464-474)."""
+        self._ensure_vib()
+        f = np.asarray(self.freq if self.freq is not None else np.zeros(0), dtype=float).ravel()
+        if self.state_type == 'gas':
+            if self.shape is None:
+                self.get_atoms()
+            ntrunc = self.shape
+        elif self.state_type == 'TS' and len(self.i_freq if self.i_freq is not None else []) == 0:
+            ntrunc = 1
+        else:
+            ntrunc = 0
+        return f[0:f.shape[0] - ntrunc]
+
+    def calc_zpe(self, verbose=False):
+        """state.py:455-476"""
+        if self.Gzpe is None:
+            self.Gzpe = 0.5 * h * float(np.sum(self.use_freq())) * JtoeV
+
+    def rot_inertia(self):
+        """sqrt(prod of non-zero principal moments) in kg m^2 (state.py:539-547)."""
+        from ..constants.physical_constants import amuA2tokgm2
+        I = np.asarray(self.inertia, dtype=float) * amuA2tokgm2
+        if self.shape == 2:
+            return float(np.sqrt(np.prod([i for i in I if i != 0])))
+        return float(np.sqrt(np.prod(I)))
+
+    # -- symbolic energies -----------------------------------------------------
+    def elec_form(self):
+        self.calc_electronic_energy()
+        return as_form(self.Gelec)
+
+    def vib_form(self):
+        if self.Gvibr is not None:
+            return as_form(self.Gvibr)
+        uf = self.use_freq()
+        self.calc_zpe()
+        if np.sum(uf) != 0.0:
+            return feature_form('vib', self)
+        return as_form(self.Gzpe if self.Gzpe is not None else 0.0)
+
+    def tran_form(self):
+        if self.Gtran is not None:
+            g = as_form(self.Gtran)
+        elif self.state_type == 'gas':
+            if self.mass is None:
+                self.get_atoms()
+            g = feature_form('tran', self)
+        else:
+            g = as_form(0.0)
+        if self.gasdata is not None:
+            for frac, st in zip(self.gasdata['fraction'], self.gasdata['state']):
+                g = g + frac * st.tran_form()
+        return g
+
+    def rot_form(self):
+        if self.Grota is not None:
+            g = as_form(self.Grota)
+        elif self.state_type == 'gas':
+            if self.inertia is None or self.shape is None:
+                self.get_atoms()
+            g = feature_form('rot', self)
+        else:
+            g = as_form(0.0)
+        if self.gasdata is not None:
+            for frac, st in zip(self.gasdata['fraction'], self.gasdata['state']):
+                g = g + frac * st.rot_form()
+        return g
+
+    def free_form(self):
+        """state.py:556-575 as a LinearForm (eV)."""
+        add = self.add_to_energy or 0.0
+        if self.Gfree is not None:
+            return as_form(self.Gfree) + add
+        return self.elec_form() + self.tran_form() + self.rot_form() + self.vib_form() + add
+
+    # -- numeric getters (one condition, evaluated on the device) --------------
+    def get_free_energy(self, T, p, verbose=False):
+        from ..engine import evaluate_forms
+        return evaluate_forms([self.free_form()], T, p, states=[self])[0]
+
+    def get_potential_energy(self, verbose=False):
+        """Electronic energy; a LinearForm when it depends on descriptors."""
+        e = self.elec_form()
+        return float(e) if e.is_constant() else e
+
+    def set_energy_modifier(self, modifier):
+        self.add_to_energy = modifier
+
+
+class ScalingState(State):
+    """Mirror of pycatkin.classes.state.ScalingState (state.py:655-779)."""
+
+    def __init__(self, state_type=None, name=None, path=None, vibs_path=None, sigma=None,
+                 mass=None, inertia=None, gasdata=None, add_to_energy=None, path_to_pickle=None,
+                 read_from_alternate=None, truncate_freq=True, energy_source=None, freq_source=None,
+                 freq=None, i_freq=None, Gelec=None, Gzpe=None, Gvibr=None, Gtran=None, Grota=None, Gfree=None,
+                 scaling_coeffs=None, scaling_reactions=None, dereference=False,
+                 use_descriptor_as_reactant=False):
+        super().__init__(state_type=state_type, name=name, path=path, vibs_path=vibs_path, sigma=sigma,
+                         mass=mass, inertia=inertia, gasdata=gasdata, add_to_energy=add_to_energy,
+                         path_to_pickle=path_to_pickle, read_from_alternate=read_from_alternate,
+                         truncate_freq=truncate_freq, energy_source=energy_source, freq_source=freq_source,
+                         freq=freq, i_freq=i_freq, Gelec=Gelec, Gzpe=Gzpe, Gvibr=Gvibr, Gtran=Gtran,
+                         Grota=Grota, Gfree=Gfree)
+        self.scaling_coeffs = scaling_coeffs
+        self.scaling_reactions = scaling_reactions
+        self.dereference = dereference
+        self.use_descriptor_as_reactant = use_descriptor_as_reactant
+
+    def _gradient(self, idx):
+        g = self.scaling_coeffs['gradient']
+        return g[idx] if isinstance(g, (list, tuple, np.ndarray)) else g
+
+    def elec_form(self):
+        """state.py:679-706 (a scalar gradient applies to every scaling reaction)."""
+        assert self.scaling_reactions is not None and self.scaling_coeffs is not None
+        e = as_form(self.scaling_coeffs['intercept'])
+        for idx, r in enumerate(self.scaling_reactions.values()):
+            rxn = r['reaction']
+            dEIS = rxn.energy_forms()['dErxn']
+            ref = sum((s.elec_form() for s in rxn.reactants), as_form(0.0)) if self.dereference else 0.0
+            e = e + r.get('multiplicity', 1.0) * (self._gradient(idx) * dEIS + ref)
+        self.Gelec = e if not e.is_constant() else float(e)
+        return e
+
+    def free_form(self):
+        """state.py:708-754"""
+        if not self.use_descriptor_as_reactant:
+            return super().free_form()
+        g = as_form(0.0)
+        for r in self.scaling_reactions.values():
+            rxn = r['reaction']
+            en = rxn.energy_forms()
+            if self.dereference:
+                refE = sum((s.elec_form() for s in rxn.reactants), as_form(0.0))
+                refG = sum((s.free_form() for s in rxn.reactants), as_form(0.0))
+            else:
+                refE = refG = 0.0
+            g = g + r.get('multiplicity', 1.0) * (-refE - en['dErxn'] + en['dGrxn'] + refG)
+        return g + self.elec_form() + (self.add_to_energy or 0.0)

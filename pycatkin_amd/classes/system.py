@@ -1,0 +1,384 @@
+"""System: the reference's System API on top of the batched device solver.
+
+Reference-API methods (pycatkin/classes/old_system.py -- the API every example
+driver uses -- and the steady-state helpers of the patched
+pycatkin/classes/system.py) are kept with their names and argument meaning.
+Each of them is a batch of one through the same C-ABI the batched methods
+(`*_batch`) use; there is no CPU compute path.
+"""
+from __future__ import annotations
+
+import copy
+from typing import NamedTuple
+
+import numpy as np
+
+from ..constants.physical_constants import R, bartoPa, eVtokJ, h, kB
+from ..energy import LinearForm
+from .reaction import Reaction
+from .reactor import InfiniteDilutionReactor, Reactor
+from .state import State
+
+
+class SteadyStateResults(NamedTuple):
+    """system.py:20-30"""
+    x: np.ndarray
+    success: bool
+
+
+class System:
+    """Holds states, reactions and a reactor; solves batches of MK models.
+
+    formulation: 'classic' (old_system.py, default) or 'patched' (system.py).
+    rate_model:  'classic' (thermodynamic reverse rate for non-activated
+                 adsorption/desorption -- what the reference's goldens pin) or
+                 'patched' (kads/kdes, reaction.py:135-162)."""
+
+    def __init__(self, times=None, start_state=None, inflow_state=None, T=293.15, p=101325.0,
+                 use_jacobian=True, ode_solver='solve_ivp', nsteps=1e4, rtol=1e-8, atol=1e-10,
+                 xtol=1e-8, ftol=1e-8, verbose=False, y0=None, min_tol=1e-32,
+                 formulation='classic', rate_model='classic', path_to_pickle=None):
+        if path_to_pickle:
+            raise NotImplementedError('pickled systems are not loaded (no unpickling of external files)')
+        self.states = dict()
+        self.unique_states = set()
+        self.reactions = dict()
+        self.reactor = None
+        self.energy_landscapes = None
+        self.formulation = formulation
+        self.rate_model = rate_model
+        self.min_tol = min_tol
+        self.snames = None
+        self.solution = None
+        self.times = None
+        self.full_steady = None
+        self.rates = None
+        self.rate_constants = None
+        self._plans = {}
+        self.set_parameters(times=times, start_state=start_state, inflow_state=inflow_state, T=T, p=p,
+                            use_jacobian=use_jacobian, ode_solver=ode_solver, nsteps=nsteps, rtol=rtol, atol=atol,
+                            xtol=xtol, ftol=ftol, verbose=verbose)
+
+    # -- setup (old_system.py:49-175, system.py:90-187) ------------------------
+    def set_parameters(self, times=None, start_state=None, inflow_state=None, T=293.15, p=101325.0,
+                       use_jacobian=True, ode_solver='solve_ivp', nsteps=1e4, rtol=1e-8, atol=1e-10,
+                       xtol=1e-8, ftol=1e-8, verbose=False):
+        self.params = dict(times=copy.deepcopy(times), start_state=copy.deepcopy(start_state),
+                           inflow_state=copy.deepcopy(inflow_state), temperature=T, pressure=p, rtol=rtol,
+                           atol=atol, xtol=xtol, ftol=ftol, jacobian=use_jacobian, nsteps=int(nsteps),
+                           ode_solver=ode_solver, verbose=verbose)
+
+    # patched-API attribute names
+    @property
+    def T(self):
+        return self.params['temperature']
+
+    @T.setter
+    def T(self, v):
+        self.params['temperature'] = v
+
+    @property
+    def p(self):
+        return self.params['pressure']
+
+    @p.setter
+    def p(self, v):
+        self.params['pressure'] = v
+
+    @property
+    def start_state(self):
+        return self.params['start_state'] or {}
+
+    @property
+    def inflow_state(self):
+        return self.params['inflow_state'] or {}
+
+    def add_state(self, state):
+        assert isinstance(state, State), 'state %s MUST be an instance of State' % state
+        if state.name in self.unique_states:
+            raise ValueError('Found two copies of state %s. State names must be unique!' % state.name)
+        self.unique_states.add(state.name)
+        self.states[state.name] = state
+        self.snames = sorted(self.states)
+        self._plans.clear()
+
+    def add_reaction(self, reaction):
+        assert isinstance(reaction, Reaction), 'reaction %s MUST be an instance of Reaction' % reaction
+        self.reactions[reaction.name] = reaction
+        self._plans.clear()
+
+    def add_reactor(self, reactor):
+        assert isinstance(reactor, Reactor)
+        self.reactor = reactor
+        self._plans.clear()
+
+    def add_energy_landscape(self, energy_landscape):
+        if self.energy_landscapes is None:
+            self.energy_landscapes = dict()
+        self.energy_landscapes[energy_landscape.name] = energy_landscape
+
+    def names_to_indices(self):
+        """old_system.py:99-152 index bookkeeping (kept for API compatibility)."""
+        self.snames = sorted(self.states)
+        ads, gas = set(), set()
+        for r in self.reactions.values():
+            for s in r.reactants + r.products:
+                if s.state_type in ('adsorbate', 'surface'):
+                    ads.add(self.snames.index(s.name))
+                elif s.state_type == 'gas':
+                    gas.add(self.snames.index(s.name))
+        self.adsorbate_indices = sorted(ads)
+        self.gas_indices = sorted(gas)
+        n = len(self.snames)
+        if self.reactor is not None:
+            self.reactor.set_indices([1 if i in ads else 0 for i in range(n)], [1 if i in gas else 0 for i in range(n)])
+            self.dynamic_indices = self.reactor.get_dynamic_indices(self.adsorbate_indices, self.gas_indices)
+
+    build = names_to_indices
+
+    # -- patched-formulation bookkeeping (system.py:191-328) -------------------
+    def index_map_ordered(self):
+        ads = [n for n, s in self.states.items() if s.state_type == 'adsorbate']
+        gas = sorted(n for n, s in self.states.items() if s.state_type == 'gas')
+        surf = sorted(n for n, s in self.states.items() if s.state_type == 'surface')
+        order = list(gas)
+        self.coverage_map = {}
+        for sf in surf:
+            grp = [sf] + [a for a in ads if a[0] == sf]
+            self.coverage_map[sf] = grp
+            order += grp
+        return order
+
+    def initial_vector(self):
+        """system.py:282-328: normalised gas fractions and site coverages, capped at min_tol."""
+        order = self.index_map_ordered()
+        pos = {s: i for i, s in enumerate(order)}
+        y = np.zeros(len(order))
+        for d in (self.start_state, self.inflow_state):
+            for k, v in d.items():
+                y[pos[k]] = v
+        gi = [pos[s] for s in order if self.states[s].state_type == 'gas']
+        if gi:
+            y[gi] /= np.sum(y[gi])
+        for grp in self.coverage_map.values():
+            ii = [pos[s] for s in grp]
+            y[ii] /= np.sum(y[ii])
+        return np.where(y < self.min_tol, self.min_tol, y)
+
+    def start_state_values(self):
+        return dict(self.start_state)
+
+    def inflow_state_values(self):
+        return dict(self.inflow_state)
+
+    # -- compilation -------------------------------------------------------------
+    def plan(self, tof_terms=(), descriptors=None):
+        from ..network import compile_system
+        key = (tuple(tof_terms), tuple(descriptors) if descriptors else None, self.formulation, self.rate_model,
+               self._energy_key())
+        if key not in self._plans:
+            if self.snames is None:
+                self.snames = sorted(self.states)
+            plan = compile_system(self, tof_terms=tof_terms, descriptors=descriptors, rate_model=self.rate_model)
+            self._plans[key] = [plan, None]
+        return self._plans[key][0]
+
+    def device(self, tof_terms=(), descriptors=None):
+        from ..engine import DeviceNetwork
+        plan = self.plan(tof_terms, descriptors)
+        key = [k for k, v in self._plans.items() if v[0] is plan][0]
+        if self._plans[key][1] is None:
+            self._plans[key][1] = DeviceNetwork.from_plan(plan)
+        return self._plans[key][1]
+
+    def _energy_key(self):
+        """User energies may be mutated between calls (volcano drivers): key the cache on them."""
+        out = []
+        for r in self.reactions.values():
+            for a in ('dErxn_user', 'dEa_fwd_user', 'dEa_rev_user', 'dGrxn_user', 'dGa_fwd_user', 'dGa_rev_user'):
+                v = getattr(r, a, None)
+                out.append(repr(v) if isinstance(v, LinearForm) else v)
+        return tuple(out)
+
+    # -- batch inputs --------------------------------------------------------------
+    def _inputs(self, net, plan, n, T, p, desc, y0, fix, inflow):
+        T = self.params['temperature'] if T is None else T
+        p = self.params['pressure'] if p is None else p
+        d = None
+        if plan.descriptors:
+            if desc is None:
+                raise ValueError('network depends on descriptors %s' % plan.descriptors)
+            cols = [np.broadcast_to(np.asarray(desc[k], float), (n,)) for k in plan.descriptors]
+            d = np.stack(cols)
+        if fix is None:
+            if plan.formulation == 'patched':
+                pp = np.broadcast_to(np.asarray(p, float), (n,))
+                fix = plan.fix_default[:, None] * pp[None, :] if len(plan.fix) else None
+            else:
+                fix = plan.fix_default * plan.fix_conc_factor
+        else:
+            fix = np.asarray(fix, float) * (plan.fix_conc_factor[:, None] if np.ndim(fix) == 2 else plan.fix_conc_factor)
+        y0 = plan.y0_default if y0 is None else y0
+        inflow = plan.inflow_default if inflow is None else inflow
+        return T, p, d, fix, y0, inflow
+
+    @staticmethod
+    def _n(*xs):
+        sizes = [int(np.size(x)) for x in xs if x is not None and np.ndim(x) > 0]
+        return max(sizes) if sizes else 1
+
+    # -- batched entry points ------------------------------------------------------
+    def rate_constants_batch(self, T=None, p=None, desc=None):
+        """kf, kr [active reactions, n] (reaction.py:94 for every condition)."""
+        plan = self.plan((), None)
+        net = self.device((), None)
+        n = self._n(T, p, *(desc or {}).values()) if desc else self._n(T, p)
+        T, p, d, _, _, _ = self._inputs(net, plan, n, T, p, desc, None, None, None)
+        kf, kr = net.rate_constants(n, T, p, d)
+        return kf.cpu().numpy(), kr.cpu().numpy()
+
+    def solve_batch(self, T=None, p=None, desc=None, y0=None, fix=None, inflow=None, tof_terms=(),
+                    steady=False, activity=False, t_end=None, t0=None, rtol=None, atol=None, max_steps=200000,
+                    newton_iters=30, to_numpy=True):
+        """Transient solve to t_end (solve_odes), optionally polished to the
+        steady state (find_steady), with TOF or activity per condition."""
+        plan = self.plan(tuple(tof_terms), None)
+        net = self.device(tuple(tof_terms), None)
+        sizes = [T, p] + (list(desc.values()) if desc else [])
+        n = self._n(*sizes)
+        if y0 is not None and np.ndim(y0) == 2:
+            n = max(n, np.shape(y0)[1])
+        T, p, d, fx, y0, inflow = self._inputs(net, plan, n, T, p, desc, y0, fix, inflow)
+        times = self.params['times'] or [0.0, 1.0e4]
+        out = net.solve(n, T, p, y0, d, fx, inflow,
+                        t0=times[0] if t0 is None else t0, t_end=times[-1] if t_end is None else t_end,
+                        rtol=self.params['rtol'] if rtol is None else rtol,
+                        atol=self.params['atol'] if atol is None else atol,
+                        max_steps=max_steps, newton=steady, newton_iters=newton_iters, activity=activity)
+        if to_numpy:
+            return {k: v.cpu().numpy() for k, v in out.items()}
+        return out
+
+    def drc_batch(self, tof_terms, T=None, p=None, desc=None, eps=1.0e-3, steady=False, t_end=None, rtol=None,
+                  atol=None, max_steps=200000):
+        """Degree of rate control of every reaction (old_system.py:490-515) for a batch.
+
+        Returns {reaction name: xi [n]} (ghost reactions: 0) plus 'tof0' and 'status'."""
+        plan = self.plan(tuple(tof_terms), None)
+        net = self.device(tuple(tof_terms), None)
+        n = self._n(T, p, *(desc.values() if desc else []))
+        T, p, d, fx, y0, inflow = self._inputs(net, plan, n, T, p, desc, None, None, None)
+        times = self.params['times'] or [0.0, 1.0e4]
+        r = net.drc(n, T, p, y0, d, fx, inflow, t0=times[0], t_end=times[-1] if t_end is None else t_end,
+                    rtol=self.params['rtol'] if rtol is None else rtol,
+                    atol=self.params['atol'] if atol is None else atol, max_steps=max_steps, newton=steady,
+                    drc_eps=eps)
+        xi = r['xi'].cpu().numpy()
+        out = {name: (xi[plan.reactions.index(name)] if name in plan.reactions else np.zeros(n))
+               for name in plan.all_reactions}
+        out['tof0'] = r['tof0'].cpu().numpy()
+        out['status'] = r['status'].cpu().numpy()
+        return out
+
+    # -- reference API (one condition) -------------------------------------------------
+    def _full(self, plan, ydyn):
+        """Dynamic state -> vector over all states in reference order."""
+        order = plan.species
+        y = np.zeros(len(order))
+        pos = {s: i for i, s in enumerate(order)}
+        if plan.formulation == 'patched':
+            y[:] = self.initial_vector()
+        else:
+            for s, v in (self.start_state or {}).items():
+                y[pos[s]] = v
+        for i, s in enumerate(plan.dyn):
+            y[pos[s]] = ydyn[i]
+        return y
+
+    def solve_odes(self):
+        """old_system.py:315-383: integrate params['times'][0] -> [-1] (final state kept)."""
+        plan = self.plan()
+        r = self.solve_batch(T=[self.params['temperature']])
+        self._check(r['status'][0], 'solve_odes')
+        self.times = np.array([self.params['times'][0], self.params['times'][-1]])
+        self.solution = np.stack([self._full(plan, plan.y0_default), self._full(plan, r['y'][:, 0])])
+        return self.solution
+
+    def find_steady(self, store_steady=False, plot_comparison=False, path=None):
+        """old_system.py:385-468: steady state from the transient end (or from the
+        start state when no transient was run)."""
+        plan = self.plan()
+        if self.solution is not None:
+            pos = {s: i for i, s in enumerate(plan.species)}
+            y0 = np.array([self.solution[-1][pos[s]] for s in plan.dyn])
+        else:
+            y0 = plan.y0_default
+        r = self.solve_batch(T=[self.params['temperature']], y0=y0[:, None], t_end=self.params['times'][0],
+                             t0=self.params['times'][0], steady=True)
+        self._check(r['status'][0], 'find_steady')
+        full = self._full(plan, r['y'][:, 0])
+        if store_steady:
+            self.full_steady = full
+        return full
+
+    @staticmethod
+    def _check(st, what):
+        if st != 0:
+            raise RuntimeError('%s: device solver status %d (1 max steps, 2 step failure, 3 non-finite, '
+                               '4 Newton failure)' % (what, st))
+
+    def reaction_terms(self, y):
+        """old_system.py:202-225: rates (n_reactions, 2) at the full state y."""
+        plan = self.plan()
+        kf, kr = self.rate_constants_batch(T=[self.params['temperature']])
+        pos = {s: i for i, s in enumerate(plan.species)}
+        y = np.asarray(y, float).ravel()
+        self.rates = np.zeros((len(plan.all_reactions), 2))
+        for j, name in enumerate(plan.all_reactions):
+            if name not in plan.reactions:
+                continue
+            a = plan.reactions.index(name)
+            rx = self.reactions[name]
+            rf, rr = kf[a, 0], kr[a, 0]
+            for side, acc in ((rx.reactants, 0), (rx.products, 1)):
+                v = rf if acc == 0 else rr
+                for s in side:
+                    if s.name in pos:
+                        c = y[pos[s.name]]
+                        if s.state_type == 'gas':
+                            c = c * (bartoPa if plan.formulation == 'classic' else self.params['pressure'])
+                        v *= c
+                if acc == 0:
+                    rf = v
+                else:
+                    rr = v
+            self.rates[j] = (rf, rr)
+        return self.rates
+
+    def run_and_return_tof(self, tof_terms, ss_solve=False):
+        """old_system.py:470-488"""
+        r = self.solve_batch(T=[self.params['temperature']], tof_terms=tuple(tof_terms), steady=ss_solve)
+        self._check(r['status'][0], 'run_and_return_tof')
+        return float(r['tof'][0])
+
+    def activity(self, tof_terms, ss_solve=False):
+        """old_system.py:517-529 (eV)"""
+        r = self.solve_batch(T=[self.params['temperature']], tof_terms=tuple(tof_terms), steady=ss_solve,
+                             activity=True)
+        self._check(r['status'][0], 'activity')
+        return float(r['tof'][0])
+
+    def degree_of_rate_control(self, tof_terms, ss_solve=False, eps=1.0e-3):
+        """old_system.py:490-515"""
+        r = self.drc_batch(tof_terms, T=[self.params['temperature']], eps=eps, steady=ss_solve)
+        self._check(r['status'][0], 'degree_of_rate_control')
+        return {k: float(r[k][0]) for k in self.reactions}
+
+    # patched-API steady state (system.py:566-639)
+    def find_steady_state(self, max_iters=30, y0=None, method=None):
+        plan = self.plan()
+        yd = plan.y0_default if y0 is None else np.asarray(y0, float)[len(plan.fix):]
+        r = self.solve_batch(T=[self.params['temperature']], y0=np.asarray(yd)[:, None],
+                             t0=0.0, t_end=0.0, steady=True)
+        x = np.concatenate([plan.fix_default, r['y'][:, 0]])
+        return SteadyStateResults(x, bool(r['status'][0] == 0))

@@ -1,0 +1,314 @@
+// Device-side building blocks of the batched MK solver (gfx950, fp64).
+//
+// Layout: one lane = one condition.  Per-condition inputs/outputs are
+// structure-of-arrays in HBM (lane c reads element c of each row -> every
+// wave-instruction is one contiguous 512-B segment).  The network plan is
+// uniform across the grid; hipcc turns its reads into scalar loads.
+// The dynamic state, the Rosenbrock stage vectors and the dense Jacobian /
+// LU factors live in VGPRs (static indices only -- NS is a template
+// parameter); the per-lane effective rate constants live in LDS so the
+// reaction loop can stay a runtime loop over the plan.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "../../include/pycatkin_amd.h"
+
+namespace pck {
+
+// pycatkin/constants/physical_constants.py:15-23
+constexpr double kB = 1.380662e-23;
+constexpr double hP = 6.626176e-34;
+constexpr double JtoeV = 6.242e18;
+constexpr double eVtokJ = 96.485;
+constexpr double amutokg = 1.66053886e-27;
+constexpr double amuA2tokgm2 = 1.66053907e-47;
+constexpr double Rgas = 8.31446262;
+constexpr double bartoPa = 1.0e5;
+constexpr double EV2JMOL = eVtokJ * 1.0e3;
+constexpr double PI = 3.14159265358979323846;
+
+// Device view of an uploaded network (passed by value as a kernel argument).
+struct NetView {
+    int D, NTH, NREG, NRXN, NDYN, NFIX, NCONS, NTOF;
+    int nfeat;                 // 2 + D + 3*NTH + NREG
+    const int32_t* th;         // NTH x 4
+    const int32_t* reg_ptr;    // NREG+1
+    const int32_t* reg_clamp;  // NREG (1: max(v, 0))
+    const int32_t* reg_feat;   // nnz
+    const int32_t* rx;         // NRXN x 6
+    const int32_t* expf;       // NRXN x NDYN
+    const int32_t* expr;       // NRXN x NDYN
+    const int32_t* foldf;      // NRXN x NFIX
+    const int32_t* foldr;      // NRXN x NFIX
+    const int32_t* cpiv;       // NCONS
+    const int32_t* tof;        // NTOF
+    const double* thd;         // NTH x 5
+    const double* freq;
+    const double* reg_coef;
+    const double* rxd;         // NRXN x 3
+    const double* S;           // NDYN x NRXN
+    const double* dyn;         // NDYN x 4
+    const double* C;           // NCONS x NDYN
+};
+
+struct CondView {
+    int64_t n;
+    const double* T; int64_t sT;
+    const double* p; int64_t sp;
+    const double* desc; int64_t ld_desc, s_desc;
+    const double* fixc; int64_t ld_fix, s_fix;
+    const double* y0; int64_t ld_y0, s_y0;
+    const double* inflow; int64_t ld_in, s_in;
+};
+
+__device__ __forceinline__ double ipow(double c, int e) {
+    // small non-negative integer powers (stoichiometric exponents)
+    if (e == 0) return 1.0;
+    if (e == 1) return c;
+    if (e == 2) return c * c;
+    double r = c * c * c;
+    for (int k = 3; k < e; ++k) r *= c;
+    return r;
+}
+
+// ---------------------------------------------------------------------------
+// Kernel-1 body: thermochemistry features -> energy program -> k (one lane)
+// State free energies: pycatkin/classes/state.py:455-584; rate constants:
+// pycatkin/classes/reaction.py:94-168, pycatkin/functions/rate_constants.py.
+// feat: this lane's feature column base; stride = lane stride of the scratch.
+// ---------------------------------------------------------------------------
+__device__ inline void thermo_features(const NetView& nv, double T, double p,
+                                       const double* desc, int64_t ld_desc,
+                                       double* feat, int64_t fs) {
+    feat[0] = 1.0;
+    feat[fs] = T;
+    for (int k = 0; k < nv.D; ++k) feat[(2 + k) * fs] = desc[k * ld_desc];
+    const double kT = kB * T;
+    for (int s = 0; s < nv.NTH; ++s) {
+        const int kind = nv.th[4 * s + 0];
+        const int f0 = nv.th[4 * s + 1], nf = nv.th[4 * s + 2], shape = nv.th[4 * s + 3];
+        const double zpe = nv.thd[5 * s + 0], mass = nv.thd[5 * s + 1];
+        const double sigma = nv.thd[5 * s + 2], rotI = nv.thd[5 * s + 3], gvfix = nv.thd[5 * s + 4];
+        double gv = 0.0, gt = 0.0, gr = 0.0;
+        if (kind & PCK_TH_VIB) {
+            if (gvfix == gvfix) {          // Gvibr given in the input (vibr_source 'inputfile')
+                gv = gvfix;
+            } else {
+                double sl = 0.0, sf = 0.0;
+                for (int q = 0; q < nf; ++q) {
+                    const double nu = nv.freq[f0 + q];
+                    sf += nu;
+                    sl += log(1.0 - exp(-nu * hP / kT));
+                }
+                gv = (sf != 0.0) ? zpe + (kT * sl) * JtoeV : zpe;     // state.py:502-507
+            }
+        }
+        if (kind & PCK_TH_GAS) {
+            const double m = mass * amutokg;                          // state.py:518-520
+            gt = (-kT * log((kT / p) * pow(2.0 * PI * m * kT / (hP * hP), 1.5))) * JtoeV;
+            if (shape == 2) {                                         // state.py:540-547
+                gr = (-kT * log(8.0 * PI * PI * kT * rotI / (sigma * hP * hP))) * JtoeV;
+            } else {
+                gr = (-kT * log((sqrt(PI) / sigma) * pow(8.0 * PI * PI * kT / (hP * hP), 1.5) * rotI)) * JtoeV;
+            }
+        }
+        const int b = 2 + nv.D + 3 * s;
+        feat[b * fs] = gv;
+        feat[(b + 1) * fs] = gt;
+        feat[(b + 2) * fs] = gr;
+    }
+    const int rb = 2 + nv.D + 3 * nv.NTH;
+    for (int r = 0; r < nv.NREG; ++r) {
+        double v = 0.0;
+        for (int q = nv.reg_ptr[r]; q < nv.reg_ptr[r + 1]; ++q) v += nv.reg_coef[q] * feat[nv.reg_feat[q] * fs];
+        if (nv.reg_clamp[r]) v = fmax(v, 0.0);   // e.g. np.max((ETS - EIS, 0.0)) in a volcano driver
+        feat[(rb + r) * fs] = v;
+    }
+}
+
+__device__ inline void rate_constants_from_feat(const NetView& nv, double T, const double* feat, int64_t fs,
+                                                int j, double& kf, double& kr) {
+    const int* rx = nv.rx + 6 * j;
+    const int type = rx[0], rev = rx[1];
+    const int rb = 2 + nv.D + 3 * nv.NTH;
+    const double ga = rx[2] >= 0 ? feat[(rb + rx[2]) * fs] * EV2JMOL : 0.0;
+    const double grxn = rx[3] >= 0 ? feat[(rb + rx[3]) * fs] * EV2JMOL : 0.0;
+    const double erxn = rx[4] >= 0 ? feat[(rb + rx[4]) * fs] * EV2JMOL : 0.0;
+    const double RT = Rgas * T;
+    const double kads_c = nv.rxd[3 * j + 0], kdes_c = nv.rxd[3 * j + 1], kdes_e = nv.rxd[3 * j + 2];
+    // reaction.py:121: "Arrhenius" or a non-zero free-energy barrier
+    if (type == PCK_RX_ARRHENIUS || (rx[5] && ga != 0.0)) {
+        kf = (kB * T / hP) * exp(-fmax(ga, 0.0) / RT);               // karr(prefactor(T), max(dGa,0))
+        kr = rev ? kf / exp(-grxn / RT) : 0.0;                        // k_from_eq_rel(kf, keq_therm)
+        return;
+    }
+    const double ka = kads_c / sqrt(T);                               // kads: area/sqrt(2 pi m kB T)
+    switch (type) {
+    case PCK_RX_ADS_KEQ:
+        kf = ka; kr = rev ? ka / exp(-grxn / RT) : 0.0; break;
+    case PCK_RX_DES_KEQ:
+        kf = ka * exp(-grxn / RT); kr = rev ? ka : 0.0; break;
+    case PCK_RX_ADS_KDES:
+        kf = ka; kr = rev ? kdes_c * pow(T, kdes_e) * exp(erxn / RT) : 0.0; break;   // des_en = -dErxn
+    case PCK_RX_DES_KDES:
+        kf = kdes_c * pow(T, kdes_e) * exp(-erxn / RT); kr = rev ? ka : 0.0; break;
+    default:
+        kf = 0.0; kr = 0.0;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Species rates / Jacobian (dense, NS static).  pycatkin/classes/old_system.py
+// :202-313 + reactor.py rhs/jacobian, and system.py:345-508 -- both are the
+// same mass-action form once the host folds fixed species and weights into
+// the plan:  f_i = rs_i * sum_j S_ij (kf_j prod c^a - kr_j prod c^b) + fl_i (in_i - y_i)
+// with c_i = cf_i * y_i.
+// ---------------------------------------------------------------------------
+template <int NS>
+struct Lane {
+    double cf[NS], rs[NS], fl[NS], in[NS];
+};
+
+// kfs/krs: this lane's effective rate constants in LDS, stride ks.
+template <int NS>
+__device__ __forceinline__ void rhs(const NetView& nv, const Lane<NS>& L, const double* kfs, const double* krs,
+                                    int ks, const double (&y)[NS], double (&f)[NS]) {
+    double c[NS];
+#pragma unroll
+    for (int i = 0; i < NS; ++i) { c[i] = L.cf[i] * y[i]; f[i] = 0.0; }
+    const int R = nv.NRXN;
+    for (int j = 0; j < R; ++j) {
+        double rf = kfs[j * ks], rr = krs[j * ks];
+        const int* ef = nv.expf + j * NS;
+        const int* er = nv.expr + j * NS;
+#pragma unroll
+        for (int i = 0; i < NS; ++i) {
+            if (ef[i]) rf *= ipow(c[i], ef[i]);
+            if (er[i]) rr *= ipow(c[i], er[i]);
+        }
+        const double net = rf - rr;
+#pragma unroll
+        for (int i = 0; i < NS; ++i) {
+            const double s = nv.S[i * R + j];
+            if (s != 0.0) f[i] += s * net;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < NS; ++i) f[i] = L.rs[i] * f[i] + L.fl[i] * (L.in[i] - y[i]);
+}
+
+template <int NS>
+__device__ __forceinline__ void jac(const NetView& nv, const Lane<NS>& L, const double* kfs, const double* krs,
+                                    int ks, const double (&y)[NS], double (&J)[NS][NS]) {
+    double c[NS];
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+        c[i] = L.cf[i] * y[i];
+#pragma unroll
+        for (int k = 0; k < NS; ++k) J[i][k] = 0.0;
+    }
+    const int R = nv.NRXN;
+    for (int j = 0; j < R; ++j) {
+        const double kf = kfs[j * ks], kr = krs[j * ks];
+        const int* ef = nv.expf + j * NS;
+        const int* er = nv.expr + j * NS;
+        double d[NS];
+#pragma unroll
+        for (int k = 0; k < NS; ++k) {
+            double v = 0.0;
+            if (ef[k]) {
+                double t = kf * (double)ef[k] * L.cf[k] * ipow(c[k], ef[k] - 1);
+#pragma unroll
+                for (int i = 0; i < NS; ++i)
+                    if (i != k && ef[i]) t *= ipow(c[i], ef[i]);
+                v += t;
+            }
+            if (er[k]) {
+                double t = kr * (double)er[k] * L.cf[k] * ipow(c[k], er[k] - 1);
+#pragma unroll
+                for (int i = 0; i < NS; ++i)
+                    if (i != k && er[i]) t *= ipow(c[i], er[i]);
+                v -= t;
+            }
+            d[k] = v;
+        }
+#pragma unroll
+        for (int i = 0; i < NS; ++i) {
+            const double s = nv.S[i * R + j];
+            if (s != 0.0) {
+#pragma unroll
+                for (int k = 0; k < NS; ++k) J[i][k] += s * d[k];
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+#pragma unroll
+        for (int k = 0; k < NS; ++k) J[i][k] *= L.rs[i];
+        J[i][i] -= L.fl[i];
+    }
+}
+
+// In-register LU with partial pivoting (row swaps by predicated selects so
+// every register index stays static).  Returns false on a zero pivot.
+template <int NS>
+__device__ __forceinline__ bool lu(double (&A)[NS][NS], int (&piv)[NS]) {
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+        int p = k;
+        double best = fabs(A[k][k]);
+#pragma unroll
+        for (int r = k + 1; r < NS; ++r) {
+            const double a = fabs(A[r][k]);
+            if (a > best) { best = a; p = r; }
+        }
+        piv[k] = p;
+#pragma unroll
+        for (int r = k + 1; r < NS; ++r) {
+            const bool sw = (p == r);
+#pragma unroll
+            for (int q = 0; q < NS; ++q) {
+                const double a = A[k][q], b = A[r][q];
+                A[k][q] = sw ? b : a;
+                A[r][q] = sw ? a : b;
+            }
+        }
+        const double d = A[k][k];
+        ok = ok && (d != 0.0) && (d == d);
+        const double inv = 1.0 / d;
+#pragma unroll
+        for (int r = k + 1; r < NS; ++r) {
+            const double l = A[r][k] * inv;
+            A[r][k] = l;
+#pragma unroll
+            for (int q = k + 1; q < NS; ++q) A[r][q] -= l * A[k][q];
+        }
+    }
+    return ok;
+}
+
+template <int NS>
+__device__ __forceinline__ void lu_solve(const double (&A)[NS][NS], const int (&piv)[NS], double (&b)[NS]) {
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+#pragma unroll
+        for (int r = k + 1; r < NS; ++r) {
+            const bool sw = (piv[k] == r);
+            const double a = b[k], c = b[r];
+            b[k] = sw ? c : a;
+            b[r] = sw ? a : c;
+        }
+#pragma unroll
+        for (int r = k + 1; r < NS; ++r) b[r] -= A[r][k] * b[k];
+    }
+#pragma unroll
+    for (int k = NS - 1; k >= 0; --k) {
+        double v = b[k];
+#pragma unroll
+        for (int q = k + 1; q < NS; ++q) v -= A[k][q] * b[q];
+        b[k] = v / A[k][k];
+    }
+}
+
+}  // namespace pck

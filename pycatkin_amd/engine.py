@@ -1,0 +1,219 @@
+"""Device execution of a compiled network through the C-ABI.
+
+PyTorch-ROCm is used for device buffers and the current HIP stream only;
+every number is computed by the HIP kernels of libpycatkin_amd.so.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib as L
+from .constants.physical_constants import bartoPa
+
+
+def _torch():
+    import torch
+    if not torch.cuda.is_available():
+        raise RuntimeError('pycatkin_amd needs a HIP device (MI355X); torch.cuda.is_available() is False '
+                           'and there is no CPU fallback')
+    return torch
+
+
+def _stream(torch):
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _ptr(t):
+    return C.c_void_p(t.data_ptr()) if t is not None else C.c_void_p(0)
+
+
+class DeviceNetwork:
+    """A NetworkPlan uploaded to the current device (pck_network_create)."""
+
+    def __init__(self, ip, dp, plan=None):
+        self.lib = L.load()
+        self.torch = _torch()
+        self.plan = plan
+        self._ip = np.ascontiguousarray(ip, np.int32)
+        self._dp = np.ascontiguousarray(dp, np.float64)
+        h = C.c_void_p()
+        L.check(self.lib.pck_network_create(self._ip.ctypes.data_as(C.c_void_p), self._ip.size,
+                                            self._dp.ctypes.data_as(C.c_void_p), self._dp.size, C.byref(h)))
+        self.h = h
+        dims = (C.c_int32 * 9)()
+        L.check(self.lib.pck_network_dims(self.h, dims))
+        (self.D, self.NTH, self.NREG, self.NRXN, self.NDYN, self.NFIX, self.NCONS, self.NTOF,
+         self.nfeat) = list(dims)
+
+    @classmethod
+    def from_plan(cls, plan):
+        return cls(plan.ip, plan.dp, plan)
+
+    def __del__(self):
+        try:
+            if getattr(self, 'h', None) is not None and self.h.value:
+                self.lib.pck_network_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+    # -- inputs -----------------------------------------------------------------
+    def _col(self, x, n, name):
+        """(tensor, stride): a scalar broadcasts with stride 0."""
+        torch = self.torch
+        t = torch.as_tensor(x, dtype=torch.float64, device='cuda')
+        if t.dim() == 0 or t.numel() == 1:
+            return t.reshape(1).contiguous(), 0
+        t = t.reshape(-1).contiguous()
+        if t.numel() != n:
+            raise ValueError('%s has %d entries for %d conditions' % (name, t.numel(), n))
+        return t, 1
+
+    def _mat(self, x, rows, n, name):
+        """[rows, n] matrix or a [rows] column broadcast to every condition."""
+        torch = self.torch
+        if rows == 0:
+            return torch.zeros(1, dtype=torch.float64, device='cuda'), 0, 0
+        t = torch.as_tensor(x, dtype=torch.float64, device='cuda')
+        if t.dim() == 1:
+            if t.numel() != rows:
+                raise ValueError('%s: expected %d rows' % (name, rows))
+            return t.contiguous(), 1, 0
+        if tuple(t.shape) != (rows, n):
+            raise ValueError('%s: expected shape (%d, %d), got %s' % (name, rows, n, tuple(t.shape)))
+        t = t.contiguous()
+        return t, n, 1
+
+    def conditions(self, n, T, p, desc=None, fixc=None, y0=None, inflow=None):
+        keep = []
+        c = L.Conditions()
+        c.n = int(n)
+        tT, c.sT = self._col(T, n, 'T')
+        tp, c.sp = self._col(p, n, 'p')
+        keep += [tT, tp]
+        c.T, c.p = _ptr(tT), _ptr(tp)
+        td, c.ld_desc, c.s_desc = self._mat(desc if desc is not None else np.zeros(0), self.D, n, 'descriptors')
+        tf, c.ld_fix, c.s_fix = self._mat(fixc if fixc is not None else np.zeros(0), self.NFIX, n, 'fixed species')
+        keep += [td, tf]
+        c.desc, c.fixc = _ptr(td), _ptr(tf)
+        if y0 is not None:
+            ty, c.ld_y0, c.s_y0 = self._mat(y0, self.NDYN, n, 'y0')
+            keep.append(ty)
+            c.y0 = _ptr(ty)
+        if inflow is not None:
+            ti, c.ld_in, c.s_in = self._mat(inflow, self.NDYN, n, 'inflow')
+            keep.append(ti)
+            c.inflow = _ptr(ti)
+        return c, keep
+
+    # -- kernels ------------------------------------------------------------------
+    def energies(self, n, T, p, desc=None):
+        torch = self.torch
+        c, keep = self.conditions(n, T, p, desc)
+        out = torch.empty((max(self.NREG, 1), max(n, 1)), dtype=torch.float64, device='cuda')
+        L.check(self.lib.pck_energies(self.h, C.byref(c), _ptr(out), out.shape[1], _stream(torch)))
+        return out[:self.NREG, :n]
+
+    def rate_constants(self, n, T, p, desc=None):
+        torch = self.torch
+        c, keep = self.conditions(n, T, p, desc)
+        kf = torch.empty((max(self.NRXN, 1), max(n, 1)), dtype=torch.float64, device='cuda')
+        kr = torch.empty_like(kf)
+        L.check(self.lib.pck_rate_constants(self.h, C.byref(c), _ptr(kf), _ptr(kr), kf.shape[1], _stream(torch)))
+        return kf[:self.NRXN, :n], kr[:self.NRXN, :n]
+
+    def species_rates(self, n, T, p, y, kf, kr, desc=None, fixc=None, inflow=None):
+        torch = self.torch
+        c, keep = self.conditions(n, T, p, desc, fixc, None, inflow)
+        y = torch.as_tensor(y, dtype=torch.float64, device='cuda').reshape(self.NDYN, n).contiguous()
+        kf, kr = kf.contiguous(), kr.contiguous()
+        out = torch.empty_like(y)
+        L.check(self.lib.pck_species_rates(self.h, C.byref(c), _ptr(kf), _ptr(kr), kf.shape[1], _ptr(y), n,
+                                           _ptr(out), _stream(torch)))
+        return out
+
+    def jacobian(self, n, T, p, y, kf, kr, desc=None, fixc=None, inflow=None):
+        torch = self.torch
+        c, keep = self.conditions(n, T, p, desc, fixc, None, inflow)
+        y = torch.as_tensor(y, dtype=torch.float64, device='cuda').reshape(self.NDYN, n).contiguous()
+        kf, kr = kf.contiguous(), kr.contiguous()
+        out = torch.empty((self.NDYN * self.NDYN, n), dtype=torch.float64, device='cuda')
+        L.check(self.lib.pck_jacobian(self.h, C.byref(c), _ptr(kf), _ptr(kr), kf.shape[1], _ptr(y), n,
+                                      _ptr(out), _stream(torch)))
+        return out.reshape(self.NDYN, self.NDYN, n)
+
+    @staticmethod
+    def params(t_end, t0=0.0, rtol=1e-8, atol=1e-10, max_steps=100000, newton=False, newton_iters=30,
+               activity=False, drc_eps=1e-3):
+        p = L.SolveParams()
+        p.t0, p.t_end, p.rtol, p.atol = float(t0), float(t_end), float(rtol), float(atol)
+        p.max_steps, p.newton, p.newton_iters = int(max_steps), int(bool(newton)), int(newton_iters)
+        p.want_activity, p.drc_eps = int(bool(activity)), float(drc_eps)
+        return p
+
+    def solve(self, n, T, p, y0, desc=None, fixc=None, inflow=None, want_k=False, out=None, **kw):
+        """pck_solve: returns dict(y [NS,n], tof [n] (or activity), status, nsteps)."""
+        torch = self.torch
+        c, keep = self.conditions(n, T, p, desc, fixc, y0, inflow)
+        prm = self.params(**kw)
+        if out is None:
+            out = dict(y=torch.empty((self.NDYN, n), dtype=torch.float64, device='cuda'),
+                       tof=torch.empty(n, dtype=torch.float64, device='cuda'),
+                       status=torch.empty(n, dtype=torch.int32, device='cuda'),
+                       nsteps=torch.empty(n, dtype=torch.int32, device='cuda'))
+            if want_k:
+                out['kf'] = torch.empty((self.NRXN, n), dtype=torch.float64, device='cuda')
+                out['kr'] = torch.empty_like(out['kf'])
+        o = L.Outputs()
+        o.y, o.ld_y = _ptr(out['y']), n
+        o.tof, o.status, o.nsteps = _ptr(out['tof']), _ptr(out['status']), _ptr(out['nsteps'])
+        if 'kf' in out:
+            o.kf, o.kr, o.ld_k = _ptr(out['kf']), _ptr(out['kr']), n
+        L.check(self.lib.pck_solve(self.h, C.byref(c), C.byref(prm), C.byref(o), _stream(torch)))
+        return out
+
+    def drc(self, n, T, p, y0, desc=None, fixc=None, inflow=None, **kw):
+        torch = self.torch
+        c, keep = self.conditions(n, T, p, desc, fixc, y0, inflow)
+        prm = self.params(**kw)
+        xi = torch.zeros((max(self.NRXN, 1), n), dtype=torch.float64, device='cuda')
+        tof0 = torch.empty(n, dtype=torch.float64, device='cuda')
+        st = torch.zeros(n, dtype=torch.int32, device='cuda')
+        L.check(self.lib.pck_drc(self.h, C.byref(c), C.byref(prm), _ptr(xi), n, _ptr(tof0), _ptr(st),
+                                 _stream(torch)))
+        return dict(xi=xi[:self.NRXN], tof0=tof0, status=st)
+
+
+_form_cache = {}
+
+
+def evaluate_forms(forms, T, p, states=None, desc=None):
+    """Evaluate LinearForms (eV) for one condition on the device (kernel 1)."""
+    from .network import compile_forms
+    states_map = {s.name: s for s in (states or [])}
+    ip, dp, regs, dnames = compile_forms(forms, states_map)
+    net = DeviceNetwork(ip, dp)
+    if dnames and desc is None:
+        raise ValueError('forms depend on descriptors %s; pass desc=' % dnames)
+    d = None if not dnames else np.array([desc[k] for k in dnames], float)
+    vals = net.energies(1, float(T), float(p), d).cpu().numpy()[:, 0]
+    return [float(vals[r]) for r in regs]
+
+
+def single_reaction_rate_constants(rxn, T, p):
+    """Reaction.calc_rate_constants for one condition through kernel (1)."""
+    from .network import NetworkPlan  # noqa: F401
+    from .classes.system import System
+    from .classes.reactor import InfiniteDilutionReactor
+    s = System()
+    seen = {}
+    for st in list(rxn.reactants) + list(rxn.products) + list(rxn.TS or []):
+        seen[st.name] = st
+    for st in seen.values():
+        s.add_state(st)
+    s.add_reaction(rxn)
+    s.add_reactor(InfiniteDilutionReactor())
+    kf, kr = s.rate_constants_batch(T=[float(T)], p=float(p))
+    return float(kf[0, 0]), float(kr[0, 0])

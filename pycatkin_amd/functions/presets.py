@@ -1,0 +1,147 @@
+"""Sweep drivers of pycatkin/functions/presets.py, batched onto the device.
+
+The reference loops over temperatures / parameter values in Python and runs
+one scipy solve per point (presets.py:31-168, 170-305); here the whole sweep
+is one launch of the batched solver (and one of the DRC kernel).
+Outputs (CSV names and columns) follow the reference.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+
+from ..constants.physical_constants import bartoPa
+
+
+def run(sim_system, steady_state_solve=False, plot_results=False, save_results=False, fig_path=None, csv_path=''):
+    """presets.py:16-28"""
+    sim_system.solve_odes()
+    if steady_state_solve:
+        sim_system.find_steady(store_steady=True)
+
+
+def _net_rates(sim_system, plan, finals, T, p=None):
+    """rates[n, n_reactions] = r_fwd - r_rev at each final state (old_system.py:202-225)."""
+    kf, kr = sim_system.rate_constants_batch(T=T, p=p)
+    pos = {s: i for i, s in enumerate(plan.species)}
+    gas_fac = bartoPa if plan.formulation == 'classic' else sim_system.params['pressure']
+    out = np.zeros((finals.shape[0], len(plan.all_reactions)))
+    for j, name in enumerate(plan.all_reactions):
+        if name not in plan.reactions:
+            continue
+        a = plan.reactions.index(name)
+        rx = sim_system.reactions[name]
+        rf, rr = kf[a].copy(), kr[a].copy()
+        for s in rx.reactants:
+            if s.name in pos:
+                rf *= finals[:, pos[s.name]] * (gas_fac if s.state_type == 'gas' else 1.0)
+        for s in rx.products:
+            if s.name in pos:
+                rr *= finals[:, pos[s.name]] * (gas_fac if s.state_type == 'gas' else 1.0)
+        out[:, j] = rf - rr
+    return out
+
+
+def _finals(sim_system, plan, ydyn, n):
+    base = sim_system._full(plan, plan.y0_default)
+    final = np.tile(base, (n, 1))
+    pos = {s: i for i, s in enumerate(plan.species)}
+    for i, s in enumerate(plan.dyn):
+        final[:, pos[s]] = ydyn[i]
+    return final
+
+
+def run_temperatures(sim_system, temperatures, steady_state_solve=False, tof_terms=None, eps=5.0e-2,
+                     plot_results=False, save_results=False, plot_transient=False, save_transient=False,
+                     fig_path=None, csv_path=''):
+    """presets.py:31-167 as one batch over `temperatures`.  Returns
+    (final [nT, n_states], rates [nT, n_reactions], drcs {T: {reaction: xi}})."""
+    temps = np.asarray(temperatures, float).ravel()
+    plan = sim_system.plan()
+    r = sim_system.solve_batch(T=temps, steady=steady_state_solve)
+    bad = np.nonzero(r['status'])[0]
+    if bad.size:
+        raise RuntimeError('device solver failed for T = %s (status %s)' % (temps[bad], r['status'][bad]))
+    final = _finals(sim_system, plan, r['y'], temps.size)
+    rates = _net_rates(sim_system, plan, final, temps)
+    drcs = {}
+    if tof_terms is not None:
+        d = sim_system.drc_batch(tof_terms, T=temps, eps=eps, steady=False)
+        for k, T in enumerate(temps):
+            drcs[T] = {name: float(d[name][k]) for name in sim_system.reactions}
+    sim_system.params['temperature'] = temps[-1]
+    if save_results:
+        _save(sim_system, plan, 'Temperature (K)', 'temperature', temps, final, rates, drcs, tof_terms, csv_path)
+    return final, rates, drcs
+
+
+def run_parameters(sim_system, parameters, params_name, steady_state_solve=False, tof_terms=None, eps=5.0e-2,
+                   plot_results=False, save_results=False, plot_transient=False, save_transient=False,
+                   fig_path=None, csv_path=''):
+    """presets.py:170-305 as one batch.  params_name: 'temperature', 'pressure',
+    'start_state_<gas>' or 'inflow_state_<gas>'."""
+    vals = np.asarray(parameters, float).ravel()
+    plan = sim_system.plan()
+    kw = {}
+    if params_name == 'temperature':
+        kw['T'] = vals
+    elif params_name == 'pressure':
+        kw['p'] = vals
+    elif params_name.startswith('start_state_'):
+        s = params_name.split('start_state_')[1]
+        if s in plan.fix:
+            fix = np.tile(plan.fix_default[:, None], (1, vals.size))
+            fix[plan.fix.index(s)] = vals
+            kw['fix'] = fix
+        else:
+            y0 = np.tile(plan.y0_default[:, None], (1, vals.size))
+            y0[plan.dyn.index(s)] = vals
+            kw['y0'] = y0
+    elif params_name.startswith('inflow_state_'):
+        s = params_name.split('inflow_state_')[1]
+        inflow = np.tile(plan.inflow_default[:, None], (1, vals.size))
+        inflow[plan.dyn.index(s)] = vals
+        kw['inflow'] = inflow
+    else:
+        raise KeyError(params_name)
+    n = vals.size
+    if 'T' not in kw:
+        kw['T'] = np.full(n, float(sim_system.params['temperature']))
+    r = sim_system.solve_batch(steady=steady_state_solve, **kw)
+    bad = np.nonzero(r['status'])[0]
+    if bad.size:
+        raise RuntimeError('device solver failed for %s = %s' % (params_name, vals[bad]))
+    final = _finals(sim_system, plan, r['y'], n)
+    rates = _net_rates(sim_system, plan, final, kw['T'], kw.get('p'))
+    drcs = {}
+    if tof_terms is not None:
+        d = sim_system.drc_batch(tof_terms, T=kw['T'], p=kw.get('p'), eps=eps)
+        for k, v in enumerate(vals):
+            drcs[v] = {name: float(d[name][k]) for name in sim_system.reactions}
+    if save_results:
+        _save(sim_system, plan, params_name, params_name, vals, final, rates, drcs, tof_terms, csv_path)
+    return final, rates, drcs
+
+
+def _save(sim_system, plan, label, stem, xs, final, rates, drcs, tof_terms, csv_path):
+    import pandas as pd
+    if csv_path and not os.path.isdir(csv_path):
+        os.makedirs(csv_path, exist_ok=True)
+    suffix = 'temperature' if stem == 'temperature' else stem
+    names = list(plan.species)
+    st = sim_system.states
+    ads = [i for i, s in enumerate(names) if st[s].state_type in ('adsorbate', 'surface') and s in plan.dyn + plan.fix]
+    gas = [i for i, s in enumerate(names) if st[s].state_type == 'gas' and s in plan.dyn + plan.fix]
+    col = np.reshape(xs, (-1, 1))
+    pd.DataFrame(np.concatenate((col, rates), axis=1), columns=[label] + list(plan.all_reactions)).to_csv(
+        csv_path + 'rates_vs_%s.csv' % suffix, index=False)
+    pd.DataFrame(np.concatenate((col, final[:, ads]), axis=1), columns=[label] + [names[i] for i in ads]).to_csv(
+        csv_path + 'coverages_vs_%s.csv' % suffix, index=False)
+    pd.DataFrame(np.concatenate((col, final[:, gas]), axis=1),
+                 columns=[label] + ['p' + names[i] + ' (bar)' for i in gas]).to_csv(
+        csv_path + 'pressures_vs_%s.csv' % suffix, index=False)
+    if tof_terms is not None:
+        vals = np.array([[x] + [drcs[x][r] for r in sim_system.reactions] for x in xs])
+        pd.DataFrame(vals, columns=[label] + list(sim_system.reactions)).to_csv(
+            csv_path + 'drcs_vs_%s.csv' % suffix, index=False)

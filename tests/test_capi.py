@@ -1,0 +1,40 @@
+"""The C-ABI library loads and exports every symbol include/pycatkin_amd.h
+declares (no compute calls: this runs without a GPU)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from pycatkin_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HDR = os.path.join(ROOT, 'include', 'pycatkin_amd.h')
+
+
+def declared_symbols():
+    txt = open(HDR).read()
+    txt = re.sub(r'/\*.*?\*/', '', txt, flags=re.S)
+    return sorted(set(re.findall(r'\b(pck_[a-z_]+)\s*\(', txt)))
+
+
+def test_header_matches_binding_table():
+    assert declared_symbols() == sorted(_lib.EXPORTED)
+
+
+@pytest.mark.skipif(not os.path.isfile(_lib.LIB_PATH), reason='library not built (run __graft_entry__.build())')
+def test_library_exports_every_declared_symbol():
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    for name in declared_symbols():
+        assert hasattr(lib, name), name
+    lib.pck_abi_version.restype = ctypes.c_int
+    assert lib.pck_abi_version() == _lib.ABI_VERSION
+
+
+def test_header_enums_match_python_constants():
+    txt = open(HDR).read()
+    assert '#define PCK_ABI_VERSION %d' % _lib.ABI_VERSION in txt
+    assert '#define PCK_MAX_DYN %d' % _lib.MAX_DYN in txt
+    enum = re.search(r'enum \{\s*PCK_I_VERSION = 0,(.*?)PCK_I_HDR', txt, re.S).group(1)
+    names = re.findall(r'(PCK_I_[A-Z_]+)', enum)
+    assert len(names) + 1 == _lib.I_HDR

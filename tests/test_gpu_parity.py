@@ -1,0 +1,198 @@
+"""HIP path (through the C-ABI) vs the CPU oracle on the same inputs.
+
+Tolerances (BASELINE north_star): steady-state coverages and log10(TOF)
+within 1e-6 relative; coverages below 1e-12 compared absolutely at 1e-15
+(they carry no weight in any rate).  Rate constants / rates / Jacobians are
+closed-form and compared at 1e-11 relative."""
+import copy
+import os
+
+import numpy as np
+import pytest
+
+from oracle import mk_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-6
+
+
+@pytest.fixture(scope='module')
+def P():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip('no HIP device')
+    import pycatkin_amd
+    return pycatkin_amd
+
+
+def volcano_sys(P, inputs, reactor=None):
+    from pycatkin_amd.functions.volcano import set_volcano_energies
+    s = P.read_from_input_file(os.path.join(inputs, 'COOxVolcano', 'input.json'))
+    if reactor is not None:
+        s.add_reactor(reactor)
+    set_volcano_energies(s)
+    return s
+
+
+def close_cov(a, b, rtol=RTOL, floor=1e-15):
+    a, b = np.asarray(a), np.asarray(b)
+    return np.all(np.abs(a - b) <= rtol * np.abs(b) + floor)
+
+
+def test_volcano_golden_point(P, inputs):
+    from pycatkin_amd.functions.volcano import volcano_activity
+    s = P.read_from_input_file(os.path.join(inputs, 'COOxVolcano', 'input.json'))
+    act, r = volcano_activity(s, [-1.0], [-1.0])
+    assert r['status'][0] == 0
+    assert abs(act[0, 0] - (-1.563)) <= 1e-3          # test/test_2.py:516
+
+
+@pytest.mark.parametrize('steady', [False, True])
+def test_volcano_grid_parity(P, inputs, steady):
+    from pycatkin_amd.functions.volcano import volcano_activity
+    be = np.linspace(-2.5, 0.5, 7)
+    s = P.read_from_input_file(os.path.join(inputs, 'COOxVolcano', 'input.json'))
+    act, r = volcano_activity(s, be, be, steady=steady)
+    assert np.all(r['status'] == 0)
+    spec = O.load_spec(os.path.join(inputs, 'COOxVolcano', 'input.json'))
+    plan = s.plan(('CO_ox',))
+    for i, eco in enumerate(be):
+        for j, eo in enumerate(be):
+            ref = O.volcano_point(spec, eco, eo, steady=True)
+            k = i * be.size + j
+            yref = np.array([ref['y'][ref['model'].idx[n]] for n in plan.dyn])
+            assert close_cov(r['y'][:, k], yref), (eco, eo, r['y'][:, k], yref)
+            assert abs(act[i, j] - ref['activity']) <= RTOL * abs(ref['activity']), (eco, eo, act[i, j], ref['activity'])
+
+
+def test_volcano_rate_constants(P, inputs):
+    s = volcano_sys(P, inputs)
+    spec = O.load_spec(os.path.join(inputs, 'COOxVolcano', 'input.json'))
+    rng = np.random.default_rng(3)
+    eco, eo = rng.uniform(-2.5, 0.5, 50), rng.uniform(-2.5, 0.5, 50)
+    T = rng.uniform(400, 800, 50)
+    kf, kr = s.rate_constants_batch(T=T, desc={'ECO': eco, 'EO': eo})
+    plan = s.plan()
+    for c in range(50):
+        sp = copy.deepcopy(spec)
+        O.set_volcano_point(sp, eco[c], eo[c], T[c])
+        rc = O.rate_constants(sp, T[c], spec['system']['p'])
+        for a, name in enumerate(plan.reactions):
+            np.testing.assert_allclose([kf[a, c], kr[a, c]], rc[name], rtol=1e-11, atol=1e-300)
+
+
+@pytest.mark.parametrize('mode', ['classic', 'patched'])
+def test_dmtm_rate_constants(P, inputs, mode):
+    s = P.read_from_input_file(os.path.join(inputs, 'DMTM', 'input.json'), rate_model=mode)
+    spec = O.load_spec(os.path.join(inputs, 'DMTM', 'input.json'))
+    T = np.linspace(350.0, 900.0, 23)
+    kf, kr = s.rate_constants_batch(T=T)
+    plan = s.plan()
+    for c, t in enumerate(T):
+        rc = O.rate_constants(spec, t, spec['system']['p'], mode)
+        for a, name in enumerate(plan.reactions):
+            np.testing.assert_allclose([kf[a, c], kr[a, c]], rc[name], rtol=1e-11, atol=1e-300)
+
+
+def test_volcano_rates_and_jacobian(P, inputs):
+    """pck_species_rates / pck_jacobian vs old_system species_odes*rowscale."""
+    s = volcano_sys(P, inputs)
+    plan = s.plan()
+    net = s.device()
+    spec = O.load_spec(os.path.join(inputs, 'COOxVolcano', 'input.json'))
+    rng = np.random.default_rng(5)
+    n = 40
+    eco, eo = rng.uniform(-2.5, 0.5, n), rng.uniform(-2.5, 0.5, n)
+    T = np.full(n, 600.0)
+    y = rng.uniform(0, 1, (plan.NS if hasattr(plan, 'NS') else len(plan.dyn), n))
+    Tt, p, d, fx, y0, inflow = s._inputs(net, plan, n, T, None, {'ECO': eco, 'EO': eo}, None, None, None)
+    kf, kr = net.rate_constants(n, Tt, p, d)
+    f = net.species_rates(n, Tt, p, y, kf, kr, d, fx, inflow).cpu().numpy()
+    J = net.jacobian(n, Tt, p, y, kf, kr, d, fx, inflow).cpu().numpy()
+    for c in range(n):
+        sp = copy.deepcopy(spec)
+        O.set_volcano_point(sp, eco[c], eo[c])
+        m = O.ClassicModel(sp)
+        full = m.y0.copy()
+        dyn = [m.idx[nm] for nm in plan.dyn]
+        full[dyn] = y[:, c]
+        np.testing.assert_allclose(f[:, c], m.rhs(full)[dyn], rtol=1e-11, atol=1e-9)
+        np.testing.assert_allclose(J[:, :, c], m.jac(full)[np.ix_(dyn, dyn)], rtol=1e-11, atol=1e-6)
+
+
+def test_volcano_cstr_parity(P, inputs):
+    """CSTReactor rows (reactor.py:141-181): gas dynamic, flow + kB*T*A/V scaling."""
+    cst = P.CSTReactor(residence_time=4.5, volume=1.8e-7, catalyst_area=3.82e-9)
+    s = volcano_sys(P, inputs, reactor=cst)
+    s.params['inflow_state'] = {'CO': 0.02, 'O2': 0.08}
+    s._plans.clear()
+    be = [(-1.0, -1.0), (-1.5, -0.5), (-0.5, -1.5)]
+    r = s.solve_batch(T=np.full(3, 600.0), desc={'ECO': [b[0] for b in be], 'EO': [b[1] for b in be]},
+                      tof_terms=('CO_ox',), steady=True, t_end=3600.0)
+    assert np.all(r['status'] == 0), r['status']
+    plan = s.plan(('CO_ox',))
+    spec = O.load_spec(os.path.join(inputs, 'COOxVolcano', 'input.json'))
+    spec['reactor'] = dict(kind='CSTR', residence_time=4.5, volume=1.8e-7, catalyst_area=3.82e-9)
+    for c, (eco, eo) in enumerate(be):
+        sp = copy.deepcopy(spec)
+        O.set_volcano_point(sp, eco, eo)
+        m = O.ClassicModel(sp, inflow_state={'CO': 0.02, 'O2': 0.08})
+        y, _ = m.solve_odes(t_end=3600.0, rtol=1e-10, atol=1e-14)
+        y = m.find_steady(y)
+        yref = np.array([y[m.idx[nm]] for nm in plan.dyn])
+        assert close_cov(r['y'][:, c], yref, floor=1e-14), (r['y'][:, c], yref)
+        assert abs(r['tof'][c] - m.tof(y, ['CO_ox'])) <= RTOL * abs(m.tof(y, ['CO_ox']))
+
+
+@pytest.mark.parametrize('eps', [1e-3, 5e-2])
+def test_volcano_drc(P, inputs, eps):
+    s = volcano_sys(P, inputs)
+    pts = [(-1.0, -1.0), (-1.5, -1.0), (-0.5, -1.5), (-2.0, -0.5)]
+    d = s.drc_batch(('CO_ox',), T=np.full(len(pts), 600.0), desc={'ECO': [a for a, b in pts], 'EO': [b for a, b in pts]},
+                    eps=eps, steady=True)
+    assert np.all(d['status'] == 0), d['status']
+    spec = O.load_spec(os.path.join(inputs, 'COOxVolcano', 'input.json'))
+    for c, (eco, eo) in enumerate(pts):
+        sp = copy.deepcopy(spec)
+        O.set_volcano_point(sp, eco, eo)
+        m = O.ClassicModel(sp)
+        xi = m.drc(['CO_ox'], eps=eps, steady=True)
+        for name, v in xi.items():
+            assert abs(d[name][c] - v) <= 1e-5 * max(1.0, abs(v)), (eco, eo, name, d[name][c], v)
+
+
+def test_full_size_properties(P, inputs):
+    """1024 x 1024 volcano grid (BASELINE configs[2] per-GPU shard): every
+    solve converges, site balance holds, and sampled points match the oracle."""
+    from pycatkin_amd.functions.volcano import volcano_activity
+    s = P.read_from_input_file(os.path.join(inputs, 'COOxVolcano', 'input.json'))
+    be = np.linspace(-2.5, 0.5, 1024)
+    act, r = volcano_activity(s, be, be, steady=True)
+    assert np.all(r['status'] == 0)
+    assert np.all(np.isfinite(act))
+    np.testing.assert_allclose(r['y'].sum(axis=0), 1.0, rtol=0, atol=1e-12)
+    spec = O.load_spec(os.path.join(inputs, 'COOxVolcano', 'input.json'))
+    rng = np.random.default_rng(11)
+    for k in rng.integers(0, be.size ** 2, 12):
+        i, j = divmod(int(k), be.size)
+        ref = O.volcano_point(spec, be[i], be[j], steady=True)['activity']
+        assert abs(act[i, j] - ref) <= RTOL * abs(ref), (be[i], be[j], act[i, j], ref)
+
+
+def test_edge_sizes(P, inputs):
+    """Empty and ragged batches; broadcast inputs."""
+    s = volcano_sys(P, inputs)
+    r0 = s.solve_batch(T=np.zeros(0) + 600.0, desc={'ECO': np.zeros(0), 'EO': np.zeros(0)}, tof_terms=('CO_ox',))
+    assert r0['y'].shape[1] in (0, 1)
+    for n in (1, 63, 129, 1000):
+        r = s.solve_batch(T=np.full(n, 600.0), desc={'ECO': np.full(n, -1.0), 'EO': np.full(n, -1.0)},
+                          tof_terms=('CO_ox',), activity=True)
+        assert np.all(r['status'] == 0)
+        assert np.allclose(r['tof'], r['tof'][0], rtol=0, atol=0)
+
+
+def test_bad_blob_is_rejected(P):
+    from pycatkin_amd.engine import DeviceNetwork
+    with pytest.raises(RuntimeError):
+        DeviceNetwork(np.zeros(5, np.int32), np.zeros(1))

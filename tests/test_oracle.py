@@ -1,0 +1,133 @@
+"""The CPU oracle against the reference's own golden values and against
+vectors produced by running the reference code (tests/golden/make_golden.py)."""
+import copy
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import mk_oracle as O
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLD = json.load(open(os.path.join(HERE, 'golden', 'ref_vectors.json')))
+
+
+def spec_of(inputs, name):
+    return O.load_spec(os.path.join(inputs, name, 'input.json'))
+
+
+def test_volcano_activity_golden(inputs):
+    """test/test_2.py:493-516 -- activity(E_CO=-1, E_O=-1) = -1.563 +- 1e-3."""
+    r = O.volcano_point(spec_of(inputs, 'COOxVolcano'), -1.0, -1.0, steady=False)
+    assert abs(r['activity'] - (-1.563)) <= 1e-3
+
+
+def test_dmtm_state_energies_golden(inputs):
+    """test/test_1.py:449-454 at 800 K.  (save_state_energies writes Grota under
+    'Translational' and Gtran under 'Rotational', presets.py:459-469.)"""
+    spec = spec_of(inputs, 'DMTM')
+    th = O.Thermo(spec, 800.0, spec['system']['p'])
+    sts = [spec['states'][s] for s in sorted(spec['states'])]
+    assert abs(max(th.free(s['name']) for s in sts) - (-7.864)) <= 1e-3
+    assert abs(max(th.vib(s) for s in sts) - 1.142) <= 1e-3
+    assert abs(min(th.tran(s) for s in sts) - (-1.259)) <= 1e-3     # 'Rotational (eV)' column
+    assert abs(min(th.rot(s) for s in sts) - (-0.659)) <= 1e-3      # 'Translational (eV)' column
+
+
+def test_dmtm_reaction_energies_golden(inputs):
+    """test/test_1.py:456-463 at 800 K (J/mol)."""
+    spec = spec_of(inputs, 'DMTM')
+    th = O.Thermo(spec, 800.0, spec['system']['p'])
+    E = [th.energies(r) for r in spec['reactions']]
+    assert abs(max(e['dErxn'] for e in E) - 220788.916) <= 1e-3
+    assert abs(max(e['dGrxn'] for e in E) - 66358.978) <= 1e-3
+    assert abs(max(e['dEa_fwd'] for e in E) - 138934.617) <= 1e-3
+    assert abs(max(e['dGa_fwd'] for e in E) - 230155.396) <= 1e-3
+
+
+def test_dmtm_transient_golden(inputs):
+    """test/test_1.py:413-419: coverages sum to 1, sCH3OH > 0.999 at t = 1e12 s."""
+    m = O.ClassicModel(spec_of(inputs, 'DMTM'))
+    y, _ = m.solve_odes(rtol=1e-8, atol=1e-12)
+    ads = m.ads_idx
+    assert abs(1 - np.sum(y[ads])) <= 1e-6
+    assert np.max(y[ads]) > 0.999
+    assert m.snames[ads[int(np.argmax(y[ads]))]] == 'sCH3OH'
+
+
+def test_dmtm_drc_golden(inputs):
+    """test/test_1.py:421-432: the rate-controlling step at 400 K is r9."""
+    m = O.ClassicModel(spec_of(inputs, 'DMTM'), T=400.0)
+    xi = m.drc(['r5', 'r9'], eps=5.0e-2, steady=True)
+    assert max(xi, key=xi.get) == 'r9'
+
+
+@pytest.mark.parametrize('mode', ['classic', 'patched'])
+def test_rate_constants_vs_reference_code(inputs, mode):
+    g = GOLD['dmtm_' + mode]
+    spec = spec_of(inputs, 'DMTM')
+    for k, T in enumerate(g['temperatures']):
+        rc = O.rate_constants(spec, T, spec['system']['p'], mode)
+        kf = np.array([rc[r][0] for r in g['reactions']])
+        kr = np.array([rc[r][1] for r in g['reactions']])
+        np.testing.assert_allclose(kf, g['kf'][k], rtol=1e-12)
+        np.testing.assert_allclose(kr, g['kr'][k], rtol=1e-12)
+
+
+@pytest.mark.parametrize('mode', ['classic', 'patched'])
+def test_species_odes_vs_reference_code(inputs, mode):
+    g = GOLD['dmtm_' + mode]
+    spec = spec_of(inputs, 'DMTM')
+    for k, T in enumerate(g['temperatures']):
+        m = O.ClassicModel(spec, T=T, mode=mode)
+        assert m.snames == g['snames']
+        dy = m.species_odes(np.array(g['odes_y'][k]))
+        np.testing.assert_allclose(dy, g['odes'][k], rtol=1e-10, atol=1e-300)
+
+
+def test_dmtm_steady_vs_reference_code(inputs):
+    """Reference solve_odes + find_steady (least_squares) vs the oracle's polished root."""
+    g = GOLD['dmtm_classic']
+    spec = spec_of(inputs, 'DMTM')
+    for k, T in enumerate(g['temperatures']):
+        m = O.ClassicModel(spec, T=T)
+        y, _ = m.solve_odes(rtol=1e-10, atol=1e-14)
+        ys = m.find_steady(y)
+        ref = np.array(g['y_steady'][k])
+        big = ref > 1e-6
+        np.testing.assert_allclose(ys[big], ref[big], rtol=1e-5)
+
+
+def test_volcano_grid_vs_reference_code(inputs):
+    """Reference old_system.activity (lsoda at rtol 1e-8 / atol 1e-10, the
+    test/test_2.py path) on a 5x5 grid vs the oracle's tight BDF transient.
+    Where the surface is steady by t = 3600 s the two agree to ~1e-14; where
+    it is not, the reference's own integration error (atol 1e-10 on coverages
+    of 1e-12..1e-20) bounds the agreement at ~1e-5 in activity."""
+    g = GOLD['volcano']
+    spec = spec_of(inputs, 'COOxVolcano')
+    for i, eco in enumerate(g['binding_energies'][:3]):
+        for j, eo in enumerate(g['binding_energies']):
+            if (eco, eo) == (-1.0, -1.5):
+                continue                           # 13 s at these tolerances; covered on the GPU
+            a = O.volcano_point(spec, eco, eo, steady=False, rtol=1e-9, atol=1e-13)['activity']
+            assert abs(a - g['activity'][i][j]) <= 2e-5 * abs(a), (eco, eo, a, g['activity'][i][j])
+
+
+def test_patched_model_runs(inputs):
+    """system.py formulation on test/CH4_input.json (BASELINE configs[0])."""
+    spec = O.load_spec(os.path.join(inputs, 'CH4', 'input.json'))
+    O.ch4_setup(spec, 1.5, 0.2)                                 # test/tests.py:206-210
+    m = O.PatchedModel(spec)
+    assert len(m.groups) == 2 and m.ngas == 8
+    z0 = np.random.default_rng(0).uniform(0.1, 1.0, len(m.y0) - m.ngas)
+    J = m.jac_ss(z0)
+    for k in (0, 3, 9):
+        eps = 1e-6 * z0[k]
+        zp, zm = z0.copy(), z0.copy()
+        zp[k] += eps
+        zm[k] -= eps
+        fd = (m.fun_ss(zp) - m.fun_ss(zm)) / (2 * eps)
+        # central differences of rates that cancel to ~1e-4 of their terms
+        np.testing.assert_allclose(J[:, k], fd, rtol=1e-3, atol=1e-6 * np.max(np.abs(J[:, k])))
