@@ -74,7 +74,7 @@ class DeviceNetwork:
     def _mat(self, x, rows, n, name):
         """[rows, n] matrix or a [rows] column broadcast to every condition."""
         torch = self.torch
-        if rows == 0:
+        if rows == 0 or x is None:
             return torch.zeros(1, dtype=torch.float64, device='cuda'), 0, 0
         t = torch.as_tensor(x, dtype=torch.float64, device='cuda')
         if t.dim() == 1:
@@ -94,8 +94,8 @@ class DeviceNetwork:
         tp, c.sp = self._col(p, n, 'p')
         keep += [tT, tp]
         c.T, c.p = _ptr(tT), _ptr(tp)
-        td, c.ld_desc, c.s_desc = self._mat(desc if desc is not None else np.zeros(0), self.D, n, 'descriptors')
-        tf, c.ld_fix, c.s_fix = self._mat(fixc if fixc is not None else np.zeros(0), self.NFIX, n, 'fixed species')
+        td, c.ld_desc, c.s_desc = self._mat(desc, self.D, n, 'descriptors')
+        tf, c.ld_fix, c.s_fix = self._mat(fixc, self.NFIX, n, 'fixed species')
         keep += [td, tf]
         c.desc, c.fixc = _ptr(td), _ptr(tf)
         if y0 is not None:

@@ -48,22 +48,35 @@ def test_volcano_golden_point(P, inputs):
     assert abs(act[0, 0] - (-1.563)) <= 1e-3          # test/test_2.py:516
 
 
-@pytest.mark.parametrize('steady', [False, True])
+@pytest.mark.parametrize('steady', [True, False])
 def test_volcano_grid_parity(P, inputs, steady):
+    """steady=True: integrate to t_end then Newton (find_steady) -- the root is
+    unique in its basin, so GPU and oracle agree to 1e-6.  steady=False: the
+    transient state at t_end = 3600 s (System.activity's semantics); where the
+    surface is still evolving the agreement is bounded by both integrators'
+    error, so both run at rtol 1e-10 / atol 1e-14 and the bar is 1e-5."""
     from pycatkin_amd.functions.volcano import volcano_activity
-    be = np.linspace(-2.5, 0.5, 7)
+    be = np.linspace(-2.5, 0.5, 5)
     s = P.read_from_input_file(os.path.join(inputs, 'COOxVolcano', 'input.json'))
-    act, r = volcano_activity(s, be, be, steady=steady)
-    assert np.all(r['status'] == 0)
+    kw = dict(rtol=1e-10, atol=1e-14)
+    act, r = volcano_activity(s, be, be, steady=steady, **kw)
+    # status 4: Newton met a degenerate root (a poisoned surface approached
+    # algebraically) and the transient end state was kept
+    assert np.all((r['status'] == 0) | (steady & (r['status'] == 4))), r['status']
+    assert np.mean(r['status'] == 4) <= 0.2          # the O-poisoned corner of the grid
     spec = O.load_spec(os.path.join(inputs, 'COOxVolcano', 'input.json'))
     plan = s.plan(('CO_ox',))
     for i, eco in enumerate(be):
         for j, eo in enumerate(be):
-            ref = O.volcano_point(spec, eco, eo, steady=True)
             k = i * be.size + j
+            ref = O.volcano_point(spec, eco, eo, steady=steady, rtol=1e-10, atol=1e-14)
+            st = steady and ref['regular']
+            if steady:      # both sides agree on which roots are regular
+                assert (r['status'][k] == 0) == ref['regular'], (eco, eo, r['status'][k])
+            tol = RTOL if st else 1e-5
             yref = np.array([ref['y'][ref['model'].idx[n]] for n in plan.dyn])
-            assert close_cov(r['y'][:, k], yref), (eco, eo, r['y'][:, k], yref)
-            assert abs(act[i, j] - ref['activity']) <= RTOL * abs(ref['activity']), (eco, eo, act[i, j], ref['activity'])
+            assert close_cov(r['y'][:, k], yref, rtol=tol, floor=1e-15 if st else 1e-13), (eco, eo, r['y'][:, k], yref)
+            assert abs(act[i, j] - ref['activity']) <= tol * abs(ref['activity']), (eco, eo, act[i, j], ref['activity'])
 
 
 def test_volcano_rate_constants(P, inputs):
@@ -169,15 +182,21 @@ def test_full_size_properties(P, inputs):
     s = P.read_from_input_file(os.path.join(inputs, 'COOxVolcano', 'input.json'))
     be = np.linspace(-2.5, 0.5, 1024)
     act, r = volcano_activity(s, be, be, steady=True)
-    assert np.all(r['status'] == 0)
+    st = r['status']
+    assert np.all((st == 0) | (st == 4))
+    assert np.mean(st == 4) < 0.15        # degenerate (O-poisoned) roots keep the transient end
     assert np.all(np.isfinite(act))
     np.testing.assert_allclose(r['y'].sum(axis=0), 1.0, rtol=0, atol=1e-12)
     spec = O.load_spec(os.path.join(inputs, 'COOxVolcano', 'input.json'))
     rng = np.random.default_rng(11)
-    for k in rng.integers(0, be.size ** 2, 12):
+    picks = list(rng.integers(0, be.size ** 2, 10)) + list(np.nonzero(st == 4)[0][:2])
+    for k in picks:
         i, j = divmod(int(k), be.size)
-        ref = O.volcano_point(spec, be[i], be[j], steady=True)['activity']
-        assert abs(act[i, j] - ref) <= RTOL * abs(ref), (be[i], be[j], act[i, j], ref)
+        ref = O.volcano_point(spec, be[i], be[j], steady=True)
+        assert (st[k] == 0) == ref['regular'], (be[i], be[j], st[k])
+        # status 4 keeps the transient end, integrated at the input's rtol 1e-8
+        tol = RTOL if ref['regular'] else 1e-4
+        assert abs(act[i, j] - ref['activity']) <= tol * abs(ref['activity']), (be[i], be[j], st[k], act[i, j], ref['activity'])
 
 
 def test_edge_sizes(P, inputs):
