@@ -183,6 +183,10 @@ def main():
     n_degen = int((st == 4).sum())
     n_fail = n - n_ok - n_degen
     steps_total = float(out['nsteps'].double().sum())
+    ns = out['nsteps'].double()
+    pad = (-n) % 64
+    wave_max = torch.nn.functional.pad(ns, (0, pad)).reshape(-1, 64).max(dim=1).values
+    lane_eff = float(ns.mean() / wave_max.mean())     # useful lane-steps / issued wave-steps
     fl = flops_per_step(plan) * steps_total
     achieved = fl / (k3_ms * 1e-3) / 1e12
 
@@ -222,7 +226,7 @@ def main():
                          'unit': 'TFLOP/s', 'frac': achieved / FP64_VECTOR_PEAK_TFLOPS, 'traffic': None,
                          'kernel': 'k_solve<4>', 'kernel_ms': k3_ms, 'rate_constants_ms': k1_ms,
                          'flops_per_launch': fl, 'flops_per_step': flops_per_step(plan),
-                         'integrator_steps': steps_total},
+                         'integrator_steps': steps_total, 'lane_efficiency': lane_eff},
             'cpu_baseline': cpu,
             'status': {'regular_root': n_ok * (world if dist else 1), 'degenerate_root_transient_kept':
                        n_degen, 'failed': n_fail},

@@ -162,12 +162,17 @@ __device__ inline void rate_constants_from_feat(const NetView& nv, double T, con
 // :202-313 + reactor.py rhs/jacobian, and system.py:345-508 -- both are the
 // same mass-action form once the host folds fixed species and weights into
 // the plan:  f_i = rs_i * sum_j S_ij (kf_j prod c^a - kr_j prod c^b) + fl_i (in_i - y_i)
-// with c_i = cf_i * y_i.
+// with c_i = cf_i * y_i,  rs_i = rs0_i + rsT_i * T.
+// cf / rs0 / rsT / fl are uniform plan data (scalar registers); the per-lane
+// pieces are T and, for flow rows, the inflow (kept in LDS beside k_eff).
 // ---------------------------------------------------------------------------
 template <int NS>
 struct Lane {
-    double cf[NS], rs[NS], fl[NS], in[NS];
+    double T;
+    const double* ins;   // this lane's inflow column in LDS (stride ks)
 };
+
+__device__ __forceinline__ double cfac(const NetView& nv, int i) { return nv.dyn[4 * i + 0]; }
 
 // kfs/krs: this lane's effective rate constants in LDS, stride ks.
 template <int NS>
@@ -175,7 +180,7 @@ __device__ __forceinline__ void rhs(const NetView& nv, const Lane<NS>& L, const 
                                     int ks, const double (&y)[NS], double (&f)[NS]) {
     double c[NS];
 #pragma unroll
-    for (int i = 0; i < NS; ++i) { c[i] = L.cf[i] * y[i]; f[i] = 0.0; }
+    for (int i = 0; i < NS; ++i) { c[i] = cfac(nv, i) * y[i]; f[i] = 0.0; }
     const int R = nv.NRXN;
     for (int j = 0; j < R; ++j) {
         double rf = kfs[j * ks], rr = krs[j * ks];
@@ -194,7 +199,11 @@ __device__ __forceinline__ void rhs(const NetView& nv, const Lane<NS>& L, const 
         }
     }
 #pragma unroll
-    for (int i = 0; i < NS; ++i) f[i] = L.rs[i] * f[i] + L.fl[i] * (L.in[i] - y[i]);
+    for (int i = 0; i < NS; ++i) {
+        const double rs0 = nv.dyn[4 * i + 1], rsT = nv.dyn[4 * i + 2], fl = nv.dyn[4 * i + 3];
+        f[i] *= (rsT != 0.0) ? rs0 + rsT * L.T : rs0;
+        if (fl != 0.0) f[i] += fl * (L.ins[i * ks] - y[i]);
+    }
 }
 
 template <int NS>
@@ -203,7 +212,7 @@ __device__ __forceinline__ void jac(const NetView& nv, const Lane<NS>& L, const 
     double c[NS];
 #pragma unroll
     for (int i = 0; i < NS; ++i) {
-        c[i] = L.cf[i] * y[i];
+        c[i] = cfac(nv, i) * y[i];
 #pragma unroll
         for (int k = 0; k < NS; ++k) J[i][k] = 0.0;
     }
@@ -217,14 +226,14 @@ __device__ __forceinline__ void jac(const NetView& nv, const Lane<NS>& L, const 
         for (int k = 0; k < NS; ++k) {
             double v = 0.0;
             if (ef[k]) {
-                double t = kf * (double)ef[k] * L.cf[k] * ipow(c[k], ef[k] - 1);
+                double t = kf * (double)ef[k] * cfac(nv, k) * ipow(c[k], ef[k] - 1);
 #pragma unroll
                 for (int i = 0; i < NS; ++i)
                     if (i != k && ef[i]) t *= ipow(c[i], ef[i]);
                 v += t;
             }
             if (er[k]) {
-                double t = kr * (double)er[k] * L.cf[k] * ipow(c[k], er[k] - 1);
+                double t = kr * (double)er[k] * cfac(nv, k) * ipow(c[k], er[k] - 1);
 #pragma unroll
                 for (int i = 0; i < NS; ++i)
                     if (i != k && er[i]) t *= ipow(c[i], er[i]);
@@ -243,9 +252,11 @@ __device__ __forceinline__ void jac(const NetView& nv, const Lane<NS>& L, const 
     }
 #pragma unroll
     for (int i = 0; i < NS; ++i) {
+        const double rs0 = nv.dyn[4 * i + 1], rsT = nv.dyn[4 * i + 2], fl = nv.dyn[4 * i + 3];
+        const double rs = (rsT != 0.0) ? rs0 + rsT * L.T : rs0;
 #pragma unroll
-        for (int k = 0; k < NS; ++k) J[i][k] *= L.rs[i];
-        J[i][i] -= L.fl[i];
+        for (int k = 0; k < NS; ++k) J[i][k] *= rs;
+        J[i][i] -= fl;
     }
 }
 
@@ -284,6 +295,7 @@ __device__ __forceinline__ bool lu(double (&A)[NS][NS], int (&piv)[NS]) {
 #pragma unroll
             for (int q = k + 1; q < NS; ++q) A[r][q] -= l * A[k][q];
         }
+        A[k][k] = inv;     // the solves multiply by the stored reciprocal (one fp64 divide per pivot)
     }
     return ok;
 }
@@ -307,7 +319,7 @@ __device__ __forceinline__ void lu_solve(const double (&A)[NS][NS], const int (&
         double v = b[k];
 #pragma unroll
         for (int q = k + 1; q < NS; ++q) v -= A[k][q] * b[q];
-        b[k] = v / A[k][k];
+        b[k] = v * A[k][k];
     }
 }
 

@@ -84,16 +84,22 @@ __global__ void __launch_bounds__(256) k_energies(NetView nv, CondView cv, doubl
 // ----------------------------------------------------------------------------
 // per-lane setup shared by the solver and the evaluation kernels
 // ----------------------------------------------------------------------------
+// LDS per lane (stride = blockDim): kf_eff[R], kr_eff[R], inflow[NS]
 template <int NS>
-__device__ __forceinline__ void lane_setup(const NetView& nv, const CondView& cv, int64_t c, Lane<NS>& L, double& T) {
+__device__ __forceinline__ void lane_setup(const NetView& nv, const CondView& cv, int64_t c, Lane<NS>& L, double& T,
+                                           double* lds_lane, int ks) {
     T = cv.T[c * cv.sT];
+    L.T = T;                          // reactor.py:34-41: CSTR row scaling is linear in T
+    double* ins = lds_lane + (size_t)2 * nv.NRXN * ks;
+    L.ins = ins;
 #pragma unroll
-    for (int i = 0; i < NS; ++i) {
-        L.cf[i] = nv.dyn[4 * i + 0];
-        L.rs[i] = nv.dyn[4 * i + 1] + nv.dyn[4 * i + 2] * T;   // reactor.py:34-41 (CSTR scaling is linear in T)
-        L.fl[i] = nv.dyn[4 * i + 3];                            // 1/residence_time for CSTR gas rows
-        L.in[i] = (L.fl[i] != 0.0 && cv.inflow) ? cv.inflow[i * cv.ld_in + c * cv.s_in] : 0.0;
+    for (int i = 0; i < NS; ++i) {    // 1/residence_time on CSTR gas rows (reactor.py:154-156)
+        if (nv.dyn[4 * i + 3] != 0.0) ins[i * ks] = cv.inflow ? cv.inflow[i * cv.ld_in + c * cv.s_in] : 0.0;
     }
+}
+
+__host__ __device__ inline size_t lds_bytes(int R, int NS, int B) {
+    return sizeof(double) * (size_t)(2 * (R > 0 ? R : 1) + NS) * B;
 }
 
 // effective k (fixed species folded in, optional DRC perturbation) -> LDS
@@ -125,7 +131,7 @@ __global__ void __launch_bounds__(128) k_species_rates(NetView nv, CondView cv, 
     double* kfs = lds + threadIdx.x;
     double* krs = lds + (size_t)nv.NRXN * blockDim.x + threadIdx.x;
     Lane<NS> L; double T;
-    lane_setup<NS>(nv, cv, c, L, T);
+    lane_setup<NS>(nv, cv, c, L, T, lds + threadIdx.x, blockDim.x);
     load_keff(nv, cv, c, kf, kr, ld_k, kfs, krs, blockDim.x, -1, 1.0);
     double yy[NS], f[NS];
 #pragma unroll
@@ -144,7 +150,7 @@ __global__ void __launch_bounds__(128) k_jacobian(NetView nv, CondView cv, const
     double* kfs = lds + threadIdx.x;
     double* krs = lds + (size_t)nv.NRXN * blockDim.x + threadIdx.x;
     Lane<NS> L; double T;
-    lane_setup<NS>(nv, cv, c, L, T);
+    lane_setup<NS>(nv, cv, c, L, T, lds + threadIdx.x, blockDim.x);
     load_keff(nv, cv, c, kf, kr, ld_k, kfs, krs, blockDim.x, -1, 1.0);
     double yy[NS], J[NS][NS];
 #pragma unroll
@@ -208,6 +214,13 @@ __device__ int integrate(const NetView& nv, const Lane<NS>& L, const double* kfs
     if (!(span > 0.0)) return PCK_ST_OK;
     double F0[NS];
     rhs<NS>(nv, L, kfs, krs, ks, y, F0);
+    double cons0[PCK_MAX_CONS];
+    for (int l = 0; l < nv.NCONS; ++l) {
+        double s = 0.0;
+#pragma unroll
+        for (int i = 0; i < NS; ++i) s += nv.C[l * NS + i] * y[i];
+        cons0[l] = s;
+    }
     // initial step (Hairer/Wanner heuristic, scipy's select_initial_step, order 4)
     double h;
     {
@@ -306,11 +319,30 @@ __device__ int integrate(const NetView& nv, const Lane<NS>& L, const double* kfs
             t = last ? t_end : t + h;
 #pragma unroll
             for (int i = 0; i < NS; ++i) y[i] = u[i];
+            // Rosenbrock stages keep linear invariants only up to the rounding of
+            // the stiff LU; rescale each non-negative site balance back onto its
+            // initial total (multiplicative, so tiny coverages keep their digits)
+            for (int l = 0; l < nv.NCONS; ++l) {
+                double s = 0.0;
+                bool pos = true;
+#pragma unroll
+                for (int i = 0; i < NS; ++i) {
+                    const double cl = nv.C[l * NS + i];
+                    pos = pos && (cl >= 0.0);
+                    s += cl * y[i];
+                }
+                if (pos && s > 0.0) {
+                    const double f = cons0[l] / s;
+#pragma unroll
+                    for (int i = 0; i < NS; ++i)
+                        if (nv.C[l * NS + i] != 0.0) y[i] *= f;
+                }
+            }
             rhs<NS>(nv, L, kfs, krs, ks, y, F0);
-            const double fac = (en > 0.0) ? 0.9 * pow(en, -0.25) : 6.0;
+            const double fac = (en > 0.0) ? 0.9 * rsqrt(sqrt(en)) : 6.0;   // 0.9 en^(-1/4)
             h *= fmin(6.0, fmax(0.2, fac));
         } else {
-            h *= finite ? fmax(0.2, 0.9 * pow(en, -0.25)) : 0.25;
+            h *= finite ? fmax(0.2, 0.9 * rsqrt(sqrt(en))) : 0.25;
         }
         if (!(h > 1e-15 * fmax(fabs(t), 1e-300)) && t < t_end) return PCK_ST_STEPFAIL;
     }
@@ -334,7 +366,8 @@ __device__ int newton(const NetView& nv, const Lane<NS>& L, const double* kfs, c
 #pragma unroll
     for (int i = 0; i < NS; ++i) z[i] = y[i];
     bool conv = false;
-    double prev = INFINITY;
+    double prev = INFINITY, lastq = 1.0;
+    int linear = 0;
     for (int it = 0; it < iters; ++it) {
         double G[NS], J[NS][NS];
         int piv[NS];
@@ -354,14 +387,37 @@ __device__ int newton(const NetView& nv, const Lane<NS>& L, const double* kfs, c
                 }
             }
         }
-        if (!lu<NS>(J, piv)) break;
+        // row equilibration: rate rows (|J| ~ k p, up to 1e9) and the O(1)
+        // conservation rows must carry comparable weight, or the LU's backward
+        // error (eps * max row norm) leaks into the site balance
 #pragma unroll
-        for (int i = 0; i < NS; ++i) G[i] = -G[i];
+        for (int i = 0; i < NS; ++i) {
+            double m = 0.0;
+#pragma unroll
+            for (int k = 0; k < NS; ++k) m = fmax(m, fabs(J[i][k]));
+            const double sc = (m > 0.0) ? 1.0 / m : 1.0;
+#pragma unroll
+            for (int k = 0; k < NS; ++k) J[i][k] *= sc;
+            G[i] = -G[i] * sc;
+        }
+        if (!lu<NS>(J, piv)) break;
         lu_solve<NS>(J, piv, G);
+        // Newton with a multiplicity estimate: after two linear steps with
+        // contraction q, step m = 1/(1-q) times (m = 2 on the halving of a
+        // near-double root); never past a zero of a decreasing component
+        double alpha = 1.0;
+        if (linear >= 2 && lastq < 0.9) {
+            alpha = fmin(4.0, 1.0 / (1.0 - lastq));
+#pragma unroll
+            for (int i = 0; i < NS; ++i)
+                if (G[i] < 0.0 && z[i] > 0.0) alpha = fmin(alpha, 0.9 * z[i] / -G[i]);
+            alpha = fmax(alpha, 1.0);
+        }
         double rel = 0.0, zmax = 0.0;
         bool finite = true;
 #pragma unroll
         for (int i = 0; i < NS; ++i) {
+            G[i] *= alpha;
             z[i] += G[i];
             finite = finite && isfinite(z[i]);
             zmax = fmax(zmax, fabs(z[i]));
@@ -376,14 +432,18 @@ __device__ int newton(const NetView& nv, const Lane<NS>& L, const double* kfs, c
         if (rel < 1e-12 || (it >= 2 && rel < 1e-7 && rel > 0.5 * prev)) { conv = true; break; }
         // linear (halving) convergence = a degenerate root, e.g. a fully
         // poisoned surface approached algebraically: keep the transient state
-        if (it >= 4 && rel > 0.25 * prev) break;
+        lastq = rel / prev;
+        linear = (rel > 0.25 * prev) ? linear + 1 : 0;
+        if (linear >= 12) break;
         prev = rel;
     }
     if (!conv) return PCK_ST_NEWTON;
-    // accept only a physical root near the transient end (no negative coverage)
+    // accept only a physical root (no negative coverage / pressure): a root
+    // with a component at -1e-30 is a vanishing species resolved below the
+    // residual's rounding, i.e. not a regular steady state
 #pragma unroll
     for (int i = 0; i < NS; ++i)
-        if (z[i] < -1e-9 * fmax(1.0, fabs(y[i]))) return PCK_ST_NEWTON;
+        if (z[i] < 0.0) return PCK_ST_NEWTON;
 #pragma unroll
     for (int i = 0; i < NS; ++i) y[i] = z[i];
     return PCK_ST_OK;
@@ -395,7 +455,7 @@ __device__ __forceinline__ double lane_tof(const NetView& nv, const Lane<NS>& L,
     // old_system.py:482-488: sum of (r_fwd - r_rev) over tof_terms
     double c[NS];
 #pragma unroll
-    for (int i = 0; i < NS; ++i) c[i] = L.cf[i] * y[i];
+    for (int i = 0; i < NS; ++i) c[i] = cfac(nv, i) * y[i];
     double tof = 0.0;
     for (int t = 0; t < nv.NTOF; ++t) {
         const int j = nv.tof[t];
@@ -432,7 +492,7 @@ __global__ void __launch_bounds__(128) k_solve(NetView nv, CondView cv, const do
         double pfac = 1.0;
         if (drc && q > 0) { pj = (q - 1) >> 1; pfac = (q & 1) ? 1.0 + a.eps : 1.0 - a.eps; }
         Lane<NS> L; double T;
-        lane_setup<NS>(nv, cv, c, L, T);
+        lane_setup<NS>(nv, cv, c, L, T, lds + threadIdx.x, blockDim.x);
         load_keff(nv, cv, c, kf, kr, ld_k, kfs, krs, blockDim.x, pj, pfac);
         double y[NS];
 #pragma unroll
@@ -661,7 +721,7 @@ extern "C" int pck_species_rates(const pck_network* net, const pck_conditions* c
     if (n == 0) return PCK_OK;
     if (!kf || !kr || !y || !dydt || ld_k < n || ld_y < n) return fail(PCK_E_ARG, "bad state/rate arrays%s", "");
     const int B = 128;
-    const size_t shm = sizeof(double) * 2 * (size_t)(net->nv.NRXN > 0 ? net->nv.NRXN : 1) * B;
+    const size_t shm = lds_bytes(net->nv.NRXN, net->nv.NDYN, B);
     dim3 g((unsigned)((n + B - 1) / B));
 #define CALL(N) hipLaunchKernelGGL(k_species_rates<N>, g, dim3(B), shm, (hipStream_t)stream, net->nv, cview(cond), kf, kr, ld_k, y, ld_y, dydt)
     PCK_NS_SWITCH(net->nv.NDYN, CALL)
@@ -678,7 +738,7 @@ extern "C" int pck_jacobian(const pck_network* net, const pck_conditions* cond, 
     if (n == 0) return PCK_OK;
     if (!kf || !kr || !y || !jo || ld_k < n || ld_y < n) return fail(PCK_E_ARG, "bad state/rate arrays%s", "");
     const int B = 128;
-    const size_t shm = sizeof(double) * 2 * (size_t)(net->nv.NRXN > 0 ? net->nv.NRXN : 1) * B;
+    const size_t shm = lds_bytes(net->nv.NRXN, net->nv.NDYN, B);
     dim3 g((unsigned)((n + B - 1) / B));
 #define CALL(N) hipLaunchKernelGGL(k_jacobian<N>, g, dim3(B), shm, (hipStream_t)stream, net->nv, cview(cond), kf, kr, ld_k, y, ld_y, jo)
     PCK_NS_SWITCH(net->nv.NDYN, CALL)
@@ -713,7 +773,7 @@ static int launch_solve(pck_network* net, const pck_conditions* cond, const pck_
     a.want_activity = prm->want_activity;
     const int B = 128;
     const int64_t lanes = n * a.G;
-    const size_t shm = sizeof(double) * 2 * (size_t)(R > 0 ? R : 1) * B;
+    const size_t shm = lds_bytes(R, net->nv.NDYN, B);
     dim3 g((unsigned)((lanes + B - 1) / B));
 #define CALL(N) hipLaunchKernelGGL(k_solve<N>, g, dim3(B), shm, s, net->nv, cview(cond), kf, kr, n, a)
     PCK_NS_SWITCH(net->nv.NDYN, CALL)

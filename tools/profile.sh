@@ -1,0 +1,20 @@
+#!/bin/bash
+# rocprofv3 runs for the bench workload: kernel trace + stats, then separate
+# PMC passes (one counter block set per pass).  Outputs under gpurun_out/$1.
+set -u
+OUT=${1:-prof}
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out/$OUT
+run() {  # name, extra rocprof args...
+  local name=$1; shift
+  timeout -k 10 150 rocprofv3 "$@" --output-format csv -d gpurun_out/$OUT/$name -o run -- \
+      python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/$OUT/$name.log 2>&1
+  local rc=$?
+  echo "$name rc=$rc" >> gpurun_out/$OUT/summary.txt
+  return $rc
+}
+run trace --kernel-trace --stats || exit $?
+run pmc_fetch --pmc FETCH_SIZE || exit $?
+run pmc_write --pmc WRITE_SIZE || exit $?
+run pmc_sq --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES || exit $?
+exit 0
