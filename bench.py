@@ -97,6 +97,8 @@ def main():
     ap.add_argument('--grid', type=int, default=1024)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-points', type=int, default=160)
+    ap.add_argument('--runtime-plan', action='store_true',
+                    help='A/B: force the runtime-plan solver instead of the compiled-in network')
     args = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -118,6 +120,8 @@ def main():
     set_volcano_energies(sim)
     plan = sim.plan(('CO_ox',))
     net = sim.device(('CO_ox',))
+    net.set_plan_mode(args.runtime_plan)
+    kernel_name = 'k_solve<PlanRT<4>>' if (args.runtime_plan or not net.compiled_plan) else 'k_solve<PlanCT<Volcano>>'
     G = args.grid
     eco_all = np.linspace(-2.5, 0.5, G * world)
     eo = np.linspace(-2.5, 0.5, G)
@@ -224,7 +228,7 @@ def main():
                        'grid_per_gpu': [G, G], 'global_grid': [G * world, G], 'parallelism': 'dp%d' % world},
             'roofline': {'bound': 'valu_fp64', 'achieved': achieved, 'peak': FP64_VECTOR_PEAK_TFLOPS,
                          'unit': 'TFLOP/s', 'frac': achieved / FP64_VECTOR_PEAK_TFLOPS, 'traffic': None,
-                         'kernel': 'k_solve<4>', 'kernel_ms': k3_ms, 'rate_constants_ms': k1_ms,
+                         'kernel': kernel_name, 'kernel_ms': k3_ms, 'rate_constants_ms': k1_ms,
                          'flops_per_launch': fl, 'flops_per_step': flops_per_step(plan),
                          'integrator_steps': steps_total, 'lane_efficiency': lane_eff},
             'cpu_baseline': cpu,

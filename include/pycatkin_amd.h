@@ -157,8 +157,12 @@ const char* pck_last_error(void);
 int pck_network_create(const int32_t* ip, int64_t n_ip, const double* dp, int64_t n_dp,
                        pck_network** out);
 int pck_network_destroy(pck_network* net);
-/* Sizes of a created network: dims[0..8] = D, NTH, NREG, NRXN, NDYN, NFIX, NCONS, NTOF, (reserved) */
+/* Sizes of a created network: dims[0..9] = D, NTH, NREG, NRXN, NDYN, NFIX, NCONS, NTOF,
+ * n_features, compiled-plan id (0 = runtime plan; see csrc/networks.h). */
 int pck_network_dims(const pck_network* net, int32_t* dims);
+/* 1: always run the runtime-plan solver even when a compiled-in plan matches
+ * the network's structural digest (for A/B checks); 0: default. */
+int pck_network_set_plan_mode(pck_network* net, int force_runtime_plan);
 
 /* Energy-program registers (eV) per condition: out[r][ld_out], r < NREG.
  * Replaces State.get_free_energy (state.py:577) / Reaction.get_reaction_energy

@@ -157,109 +157,6 @@ __device__ inline void rate_constants_from_feat(const NetView& nv, double T, con
     }
 }
 
-// ---------------------------------------------------------------------------
-// Species rates / Jacobian (dense, NS static).  pycatkin/classes/old_system.py
-// :202-313 + reactor.py rhs/jacobian, and system.py:345-508 -- both are the
-// same mass-action form once the host folds fixed species and weights into
-// the plan:  f_i = rs_i * sum_j S_ij (kf_j prod c^a - kr_j prod c^b) + fl_i (in_i - y_i)
-// with c_i = cf_i * y_i,  rs_i = rs0_i + rsT_i * T.
-// cf / rs0 / rsT / fl are uniform plan data (scalar registers); the per-lane
-// pieces are T and, for flow rows, the inflow (kept in LDS beside k_eff).
-// ---------------------------------------------------------------------------
-template <int NS>
-struct Lane {
-    double T;
-    const double* ins;   // this lane's inflow column in LDS (stride ks)
-};
-
-__device__ __forceinline__ double cfac(const NetView& nv, int i) { return nv.dyn[4 * i + 0]; }
-
-// kfs/krs: this lane's effective rate constants in LDS, stride ks.
-template <int NS>
-__device__ __forceinline__ void rhs(const NetView& nv, const Lane<NS>& L, const double* kfs, const double* krs,
-                                    int ks, const double (&y)[NS], double (&f)[NS]) {
-    double c[NS];
-#pragma unroll
-    for (int i = 0; i < NS; ++i) { c[i] = cfac(nv, i) * y[i]; f[i] = 0.0; }
-    const int R = nv.NRXN;
-    for (int j = 0; j < R; ++j) {
-        double rf = kfs[j * ks], rr = krs[j * ks];
-        const int* ef = nv.expf + j * NS;
-        const int* er = nv.expr + j * NS;
-#pragma unroll
-        for (int i = 0; i < NS; ++i) {
-            if (ef[i]) rf *= ipow(c[i], ef[i]);
-            if (er[i]) rr *= ipow(c[i], er[i]);
-        }
-        const double net = rf - rr;
-#pragma unroll
-        for (int i = 0; i < NS; ++i) {
-            const double s = nv.S[i * R + j];
-            if (s != 0.0) f[i] += s * net;
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < NS; ++i) {
-        const double rs0 = nv.dyn[4 * i + 1], rsT = nv.dyn[4 * i + 2], fl = nv.dyn[4 * i + 3];
-        f[i] *= (rsT != 0.0) ? rs0 + rsT * L.T : rs0;
-        if (fl != 0.0) f[i] += fl * (L.ins[i * ks] - y[i]);
-    }
-}
-
-template <int NS>
-__device__ __forceinline__ void jac(const NetView& nv, const Lane<NS>& L, const double* kfs, const double* krs,
-                                    int ks, const double (&y)[NS], double (&J)[NS][NS]) {
-    double c[NS];
-#pragma unroll
-    for (int i = 0; i < NS; ++i) {
-        c[i] = cfac(nv, i) * y[i];
-#pragma unroll
-        for (int k = 0; k < NS; ++k) J[i][k] = 0.0;
-    }
-    const int R = nv.NRXN;
-    for (int j = 0; j < R; ++j) {
-        const double kf = kfs[j * ks], kr = krs[j * ks];
-        const int* ef = nv.expf + j * NS;
-        const int* er = nv.expr + j * NS;
-        double d[NS];
-#pragma unroll
-        for (int k = 0; k < NS; ++k) {
-            double v = 0.0;
-            if (ef[k]) {
-                double t = kf * (double)ef[k] * cfac(nv, k) * ipow(c[k], ef[k] - 1);
-#pragma unroll
-                for (int i = 0; i < NS; ++i)
-                    if (i != k && ef[i]) t *= ipow(c[i], ef[i]);
-                v += t;
-            }
-            if (er[k]) {
-                double t = kr * (double)er[k] * cfac(nv, k) * ipow(c[k], er[k] - 1);
-#pragma unroll
-                for (int i = 0; i < NS; ++i)
-                    if (i != k && er[i]) t *= ipow(c[i], er[i]);
-                v -= t;
-            }
-            d[k] = v;
-        }
-#pragma unroll
-        for (int i = 0; i < NS; ++i) {
-            const double s = nv.S[i * R + j];
-            if (s != 0.0) {
-#pragma unroll
-                for (int k = 0; k < NS; ++k) J[i][k] += s * d[k];
-            }
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < NS; ++i) {
-        const double rs0 = nv.dyn[4 * i + 1], rsT = nv.dyn[4 * i + 2], fl = nv.dyn[4 * i + 3];
-        const double rs = (rsT != 0.0) ? rs0 + rsT * L.T : rs0;
-#pragma unroll
-        for (int k = 0; k < NS; ++k) J[i][k] *= rs;
-        J[i][i] -= fl;
-    }
-}
-
 // In-register LU with partial pivoting (row swaps by predicated selects so
 // every register index stays static).  Returns false on a zero pivot.
 template <int NS>

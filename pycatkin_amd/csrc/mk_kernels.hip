@@ -26,7 +26,17 @@ struct pck_network {
     int64_t scratch_cap = 0;
     double* kbuf = nullptr;         // kf/kr scratch for pck_solve/pck_drc
     int64_t kbuf_cap = 0;
+    int spec = 0;                   // id of the compiled-in plan (networks.h) or 0
+    int force_runtime_plan = 0;     // pck_network_set_plan_mode(net, 1): always the runtime plan
+    unsigned long long digest = 0;
 };
+
+// FNV-1a 64 over the solver-side structure (network.py: structural_digest)
+static unsigned long long fnv1a(unsigned long long h, const void* p, size_t n) {
+    const unsigned char* b = (const unsigned char*)p;
+    for (size_t i = 0; i < n; ++i) { h ^= b[i]; h *= 0x100000001b3ULL; }
+    return h;
+}
 
 static thread_local char g_err[512] = "";
 static int fail(int code, const char* fmt, const char* a = "", long long b = 0) {
@@ -81,464 +91,7 @@ __global__ void __launch_bounds__(256) k_energies(NetView nv, CondView cv, doubl
     for (int r = 0; r < nv.NREG; ++r) out[r * ld_out + c] = f[(rb + r) * fs];
 }
 
-// ----------------------------------------------------------------------------
-// per-lane setup shared by the solver and the evaluation kernels
-// ----------------------------------------------------------------------------
-// LDS per lane (stride = blockDim): kf_eff[R], kr_eff[R], inflow[NS]
-template <int NS>
-__device__ __forceinline__ void lane_setup(const NetView& nv, const CondView& cv, int64_t c, Lane<NS>& L, double& T,
-                                           double* lds_lane, int ks) {
-    T = cv.T[c * cv.sT];
-    L.T = T;                          // reactor.py:34-41: CSTR row scaling is linear in T
-    double* ins = lds_lane + (size_t)2 * nv.NRXN * ks;
-    L.ins = ins;
-#pragma unroll
-    for (int i = 0; i < NS; ++i) {    // 1/residence_time on CSTR gas rows (reactor.py:154-156)
-        if (nv.dyn[4 * i + 3] != 0.0) ins[i * ks] = cv.inflow ? cv.inflow[i * cv.ld_in + c * cv.s_in] : 0.0;
-    }
-}
-
-__host__ __device__ inline size_t lds_bytes(int R, int NS, int B) {
-    return sizeof(double) * (size_t)(2 * (R > 0 ? R : 1) + NS) * B;
-}
-
-// effective k (fixed species folded in, optional DRC perturbation) -> LDS
-__device__ __forceinline__ void load_keff(const NetView& nv, const CondView& cv, int64_t c, const double* kf,
-                                          const double* kr, int64_t ld_k, double* kfs, double* krs, int ks,
-                                          int pj, double pfac) {
-    for (int j = 0; j < nv.NRXN; ++j) {
-        double a = kf[j * ld_k + c], b = kr[j * ld_k + c];
-        for (int q = 0; q < nv.NFIX; ++q) {
-            const int ea = nv.foldf[j * nv.NFIX + q], eb = nv.foldr[j * nv.NFIX + q];
-            if (ea | eb) {
-                const double x = cv.fixc[q * cv.ld_fix + c * cv.s_fix];
-                if (ea) a *= ipow(x, ea);
-                if (eb) b *= ipow(x, eb);
-            }
-        }
-        if (j == pj) { a *= pfac; b *= pfac; }   // old_system.py:504-506: kf + eps*kf, kr*(1 + eps)
-        kfs[j * ks] = a;
-        krs[j * ks] = b;
-    }
-}
-
-template <int NS>
-__global__ void __launch_bounds__(128) k_species_rates(NetView nv, CondView cv, const double* kf, const double* kr,
-                                                       int64_t ld_k, const double* y, int64_t ld_y, double* dydt) {
-    extern __shared__ double lds[];
-    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= cv.n) return;
-    double* kfs = lds + threadIdx.x;
-    double* krs = lds + (size_t)nv.NRXN * blockDim.x + threadIdx.x;
-    Lane<NS> L; double T;
-    lane_setup<NS>(nv, cv, c, L, T, lds + threadIdx.x, blockDim.x);
-    load_keff(nv, cv, c, kf, kr, ld_k, kfs, krs, blockDim.x, -1, 1.0);
-    double yy[NS], f[NS];
-#pragma unroll
-    for (int i = 0; i < NS; ++i) yy[i] = y[i * ld_y + c];
-    rhs<NS>(nv, L, kfs, krs, blockDim.x, yy, f);
-#pragma unroll
-    for (int i = 0; i < NS; ++i) dydt[i * ld_y + c] = f[i];
-}
-
-template <int NS>
-__global__ void __launch_bounds__(128) k_jacobian(NetView nv, CondView cv, const double* kf, const double* kr,
-                                                  int64_t ld_k, const double* y, int64_t ld_y, double* jo) {
-    extern __shared__ double lds[];
-    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= cv.n) return;
-    double* kfs = lds + threadIdx.x;
-    double* krs = lds + (size_t)nv.NRXN * blockDim.x + threadIdx.x;
-    Lane<NS> L; double T;
-    lane_setup<NS>(nv, cv, c, L, T, lds + threadIdx.x, blockDim.x);
-    load_keff(nv, cv, c, kf, kr, ld_k, kfs, krs, blockDim.x, -1, 1.0);
-    double yy[NS], J[NS][NS];
-#pragma unroll
-    for (int i = 0; i < NS; ++i) yy[i] = y[i * ld_y + c];
-    jac<NS>(nv, L, kfs, krs, blockDim.x, yy, J);
-#pragma unroll
-    for (int i = 0; i < NS; ++i)
-#pragma unroll
-        for (int k = 0; k < NS; ++k) jo[(i * NS + k) * ld_y + c] = J[i][k];
-}
-
-// ----------------------------------------------------------------------------
-// kernel (3)+(4): solve
-// ----------------------------------------------------------------------------
-struct SolveArgs {
-    double t0, t_end, rtol, atol, eps;
-    int max_steps, newton, newton_iters, want_activity;
-    double* y; int64_t ld_y;
-    double* tof; int32_t* status; int32_t* nsteps;
-    double* xi; int64_t ld_xi; double* tof0;   // DRC mode
-    int G;                                     // lanes per condition (1, or DRC group size)
-};
-
-template <int NS>
-__device__ __forceinline__ double rms_scaled(const double (&e)[NS], const double (&a)[NS], const double (&b)[NS],
-                                             double atol, double rtol) {
-    double s = 0.0;
-#pragma unroll
-    for (int i = 0; i < NS; ++i) {
-        const double sc = atol + rtol * fmax(fabs(a[i]), fabs(b[i]));
-        const double r = e[i] / sc;
-        s += r * r;
-    }
-    return sqrt(s / NS);
-}
-
-// RODAS4 (Hairer & Wanner, stiffly accurate 4(3) Rosenbrock, L-stable),
-// autonomous form:  (I/(h g) - J) k_i = f(u_i) + sum_j C_ij k_j / h,
-// u_{i+1} = y + sum_j a_ij k_j,  y_new = u_5 + k5 + k6,  error = k6.
-namespace rodas4 {
-constexpr double g = 0.25;
-constexpr double a21 = 1.544, a31 = 0.9466785280815826, a32 = 0.2557011698983284;
-constexpr double a41 = 3.314825187068521, a42 = 2.896124015972201, a43 = 0.9986419139977817;
-constexpr double a51 = 1.221224509226641, a52 = 6.019134481288629, a53 = 12.53708332932087,
-                 a54 = -0.6878860361058950;
-constexpr double C21 = -5.6688, C31 = -2.430093356833875, C32 = -0.2063599157091915;
-constexpr double C41 = -0.1073529058151375, C42 = -9.594562251023355, C43 = -20.47028614809616;
-constexpr double C51 = 7.496443313967647, C52 = -10.24680431464352, C53 = -33.99990352819905,
-                 C54 = 11.70890893206160;
-constexpr double C61 = 8.083246795921522, C62 = -7.981132988064893, C63 = -31.52159432874371,
-                 C64 = 16.31930543123136, C65 = -6.058818238834054;
-}  // namespace rodas4
-
-template <int NS>
-__device__ int integrate(const NetView& nv, const Lane<NS>& L, const double* kfs, const double* krs, int ks,
-                         double (&y)[NS], double t0, double t_end, double rtol, double atol, int max_steps,
-                         int& nsteps) {
-    using namespace rodas4;
-    nsteps = 0;
-    const double span = t_end - t0;
-    if (!(span > 0.0)) return PCK_ST_OK;
-    double F0[NS];
-    rhs<NS>(nv, L, kfs, krs, ks, y, F0);
-    double cons0[PCK_MAX_CONS];
-    for (int l = 0; l < nv.NCONS; ++l) {
-        double s = 0.0;
-#pragma unroll
-        for (int i = 0; i < NS; ++i) s += nv.C[l * NS + i] * y[i];
-        cons0[l] = s;
-    }
-    // initial step (Hairer/Wanner heuristic, scipy's select_initial_step, order 4)
-    double h;
-    {
-        double d0 = 0.0, d1 = 0.0;
-#pragma unroll
-        for (int i = 0; i < NS; ++i) {
-            const double sc = atol + rtol * fabs(y[i]);
-            d0 += (y[i] / sc) * (y[i] / sc);
-            d1 += (F0[i] / sc) * (F0[i] / sc);
-        }
-        d0 = sqrt(d0 / NS); d1 = sqrt(d1 / NS);
-        double h0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : 0.01 * d0 / d1;
-        h0 = fmin(h0, span);
-        double y1[NS], F1[NS];
-#pragma unroll
-        for (int i = 0; i < NS; ++i) y1[i] = y[i] + h0 * F0[i];
-        rhs<NS>(nv, L, kfs, krs, ks, y1, F1);
-        double d2 = 0.0;
-#pragma unroll
-        for (int i = 0; i < NS; ++i) {
-            const double sc = atol + rtol * fabs(y[i]);
-            const double q = (F1[i] - F0[i]) / sc;
-            d2 += q * q;
-        }
-        d2 = sqrt(d2 / NS) / h0;
-        const double h1 = (d1 <= 1e-15 && d2 <= 1e-15) ? fmax(1e-6, h0 * 1e-3) : pow(0.01 / fmax(d1, d2), 0.2);
-        h = fmin(fmin(100.0 * h0, h1), span);
-    }
-    double t = t0;
-    double W[NS][NS];
-    int piv[NS];
-    while (t < t_end) {
-        if (nsteps >= max_steps) return PCK_ST_MAXSTEPS;
-        ++nsteps;
-        bool last = false;
-        if (t + h >= t_end) { h = t_end - t; last = true; }
-        // W = I/(h g) - J
-        jac<NS>(nv, L, kfs, krs, ks, y, W);
-        const double ig = 1.0 / (h * g);
-#pragma unroll
-        for (int i = 0; i < NS; ++i) {
-#pragma unroll
-            for (int k = 0; k < NS; ++k) W[i][k] = -W[i][k];
-            W[i][i] += ig;
-        }
-        if (!lu<NS>(W, piv)) { h *= 0.25; continue; }
-        const double ih = 1.0 / h;
-        double k1[NS], k2[NS], k3[NS], k4[NS], k5[NS], u[NS], fu[NS];
-#pragma unroll
-        for (int i = 0; i < NS; ++i) k1[i] = F0[i];
-        lu_solve<NS>(W, piv, k1);
-#pragma unroll
-        for (int i = 0; i < NS; ++i) u[i] = y[i] + a21 * k1[i];
-        rhs<NS>(nv, L, kfs, krs, ks, u, fu);
-#pragma unroll
-        for (int i = 0; i < NS; ++i) k2[i] = fu[i] + ih * (C21 * k1[i]);
-        lu_solve<NS>(W, piv, k2);
-#pragma unroll
-        for (int i = 0; i < NS; ++i) u[i] = y[i] + a31 * k1[i] + a32 * k2[i];
-        rhs<NS>(nv, L, kfs, krs, ks, u, fu);
-#pragma unroll
-        for (int i = 0; i < NS; ++i) k3[i] = fu[i] + ih * (C31 * k1[i] + C32 * k2[i]);
-        lu_solve<NS>(W, piv, k3);
-#pragma unroll
-        for (int i = 0; i < NS; ++i) u[i] = y[i] + a41 * k1[i] + a42 * k2[i] + a43 * k3[i];
-        rhs<NS>(nv, L, kfs, krs, ks, u, fu);
-#pragma unroll
-        for (int i = 0; i < NS; ++i) k4[i] = fu[i] + ih * (C41 * k1[i] + C42 * k2[i] + C43 * k3[i]);
-        lu_solve<NS>(W, piv, k4);
-#pragma unroll
-        for (int i = 0; i < NS; ++i) u[i] = y[i] + a51 * k1[i] + a52 * k2[i] + a53 * k3[i] + a54 * k4[i];
-        rhs<NS>(nv, L, kfs, krs, ks, u, fu);
-#pragma unroll
-        for (int i = 0; i < NS; ++i) k5[i] = fu[i] + ih * (C51 * k1[i] + C52 * k2[i] + C53 * k3[i] + C54 * k4[i]);
-        lu_solve<NS>(W, piv, k5);
-#pragma unroll
-        for (int i = 0; i < NS; ++i) u[i] += k5[i];
-        rhs<NS>(nv, L, kfs, krs, ks, u, fu);
-        // reuse k5's slot for k6 once it has been folded into u
-#pragma unroll
-        for (int i = 0; i < NS; ++i)
-            k5[i] = fu[i] + ih * (C61 * k1[i] + C62 * k2[i] + C63 * k3[i] + C64 * k4[i] + C65 * k5[i]);
-        lu_solve<NS>(W, piv, k5);
-        bool finite = true;
-        double s = 0.0;
-#pragma unroll
-        for (int i = 0; i < NS; ++i) {
-            u[i] += k5[i];
-            finite = finite && isfinite(u[i]) && isfinite(k5[i]);
-            const double sc = atol + rtol * fmax(fabs(y[i]), fabs(u[i]));
-            const double r = k5[i] / sc;
-            s += r * r;
-        }
-        const double en = finite ? sqrt(s / NS) : INFINITY;
-        if (en <= 1.0) {
-            t = last ? t_end : t + h;
-#pragma unroll
-            for (int i = 0; i < NS; ++i) y[i] = u[i];
-            // Rosenbrock stages keep linear invariants only up to the rounding of
-            // the stiff LU; rescale each non-negative site balance back onto its
-            // initial total (multiplicative, so tiny coverages keep their digits)
-            for (int l = 0; l < nv.NCONS; ++l) {
-                double s = 0.0;
-                bool pos = true;
-#pragma unroll
-                for (int i = 0; i < NS; ++i) {
-                    const double cl = nv.C[l * NS + i];
-                    pos = pos && (cl >= 0.0);
-                    s += cl * y[i];
-                }
-                if (pos && s > 0.0) {
-                    const double f = cons0[l] / s;
-#pragma unroll
-                    for (int i = 0; i < NS; ++i)
-                        if (nv.C[l * NS + i] != 0.0) y[i] *= f;
-                }
-            }
-            rhs<NS>(nv, L, kfs, krs, ks, y, F0);
-            const double fac = (en > 0.0) ? 0.9 * rsqrt(sqrt(en)) : 6.0;   // 0.9 en^(-1/4)
-            h *= fmin(6.0, fmax(0.2, fac));
-        } else {
-            h *= finite ? fmax(0.2, 0.9 * rsqrt(sqrt(en))) : 0.25;
-        }
-        if (!(h > 1e-15 * fmax(fabs(t), 1e-300)) && t < t_end) return PCK_ST_STEPFAIL;
-    }
-    return PCK_ST_OK;
-}
-
-// Newton on f(y) = 0 with the plan's conservation laws replacing their pivot
-// rows (old_system.py:385-468 polishes with scipy least_squares; the root it
-// converges to is the same).
-template <int NS>
-__device__ int newton(const NetView& nv, const Lane<NS>& L, const double* kfs, const double* krs, int ks,
-                      double (&y)[NS], int iters) {
-    double b[PCK_MAX_CONS];
-    for (int l = 0; l < nv.NCONS; ++l) {
-        double s = 0.0;
-#pragma unroll
-        for (int i = 0; i < NS; ++i) s += nv.C[l * NS + i] * y[i];
-        b[l] = s;
-    }
-    double z[NS];
-#pragma unroll
-    for (int i = 0; i < NS; ++i) z[i] = y[i];
-    bool conv = false;
-    double prev = INFINITY, lastq = 1.0;
-    int linear = 0;
-    for (int it = 0; it < iters; ++it) {
-        double G[NS], J[NS][NS];
-        int piv[NS];
-        rhs<NS>(nv, L, kfs, krs, ks, z, G);
-        jac<NS>(nv, L, kfs, krs, ks, z, J);
-        for (int l = 0; l < nv.NCONS; ++l) {
-            const int p = nv.cpiv[l];
-            double s = 0.0;
-#pragma unroll
-            for (int i = 0; i < NS; ++i) s += nv.C[l * NS + i] * z[i];
-#pragma unroll
-            for (int i = 0; i < NS; ++i) {
-                if (i == p) {
-                    G[i] = s - b[l];
-#pragma unroll
-                    for (int k = 0; k < NS; ++k) J[i][k] = nv.C[l * NS + k];
-                }
-            }
-        }
-        // row equilibration: rate rows (|J| ~ k p, up to 1e9) and the O(1)
-        // conservation rows must carry comparable weight, or the LU's backward
-        // error (eps * max row norm) leaks into the site balance
-#pragma unroll
-        for (int i = 0; i < NS; ++i) {
-            double m = 0.0;
-#pragma unroll
-            for (int k = 0; k < NS; ++k) m = fmax(m, fabs(J[i][k]));
-            const double sc = (m > 0.0) ? 1.0 / m : 1.0;
-#pragma unroll
-            for (int k = 0; k < NS; ++k) J[i][k] *= sc;
-            G[i] = -G[i] * sc;
-        }
-        if (!lu<NS>(J, piv)) break;
-        lu_solve<NS>(J, piv, G);
-        // Newton with a multiplicity estimate: after two linear steps with
-        // contraction q, step m = 1/(1-q) times (m = 2 on the halving of a
-        // near-double root); never past a zero of a decreasing component
-        double alpha = 1.0;
-        if (linear >= 2 && lastq < 0.9) {
-            alpha = fmin(4.0, 1.0 / (1.0 - lastq));
-#pragma unroll
-            for (int i = 0; i < NS; ++i)
-                if (G[i] < 0.0 && z[i] > 0.0) alpha = fmin(alpha, 0.9 * z[i] / -G[i]);
-            alpha = fmax(alpha, 1.0);
-        }
-        double rel = 0.0, zmax = 0.0;
-        bool finite = true;
-#pragma unroll
-        for (int i = 0; i < NS; ++i) {
-            G[i] *= alpha;
-            z[i] += G[i];
-            finite = finite && isfinite(z[i]);
-            zmax = fmax(zmax, fabs(z[i]));
-        }
-        if (!finite) break;
-        // components below 1e-12 of the largest are held to an absolute
-        // 1e-24 * zmax: their relative digits sit under the residual's rounding
-#pragma unroll
-        for (int i = 0; i < NS; ++i) rel = fmax(rel, fabs(G[i]) / fmax(fabs(z[i]), 1e-12 * zmax + 1e-300));
-        // converged: relative step at the 1e-12 level, or stagnated at the
-        // rounding level of the residual (no 2x decrease once below 1e-7)
-        if (rel < 1e-12 || (it >= 2 && rel < 1e-7 && rel > 0.5 * prev)) { conv = true; break; }
-        // linear (halving) convergence = a degenerate root, e.g. a fully
-        // poisoned surface approached algebraically: keep the transient state
-        lastq = rel / prev;
-        linear = (rel > 0.25 * prev) ? linear + 1 : 0;
-        if (linear >= 12) break;
-        prev = rel;
-    }
-    if (!conv) return PCK_ST_NEWTON;
-    // accept only a physical root (no negative coverage / pressure): a root
-    // with a component at -1e-30 is a vanishing species resolved below the
-    // residual's rounding, i.e. not a regular steady state
-#pragma unroll
-    for (int i = 0; i < NS; ++i)
-        if (z[i] < 0.0) return PCK_ST_NEWTON;
-#pragma unroll
-    for (int i = 0; i < NS; ++i) y[i] = z[i];
-    return PCK_ST_OK;
-}
-
-template <int NS>
-__device__ __forceinline__ double lane_tof(const NetView& nv, const Lane<NS>& L, const double* kfs,
-                                           const double* krs, int ks, const double (&y)[NS]) {
-    // old_system.py:482-488: sum of (r_fwd - r_rev) over tof_terms
-    double c[NS];
-#pragma unroll
-    for (int i = 0; i < NS; ++i) c[i] = cfac(nv, i) * y[i];
-    double tof = 0.0;
-    for (int t = 0; t < nv.NTOF; ++t) {
-        const int j = nv.tof[t];
-        double rf = kfs[j * ks], rr = krs[j * ks];
-#pragma unroll
-        for (int i = 0; i < NS; ++i) {
-            const int a = nv.expf[j * NS + i], b = nv.expr[j * NS + i];
-            if (a) rf *= ipow(c[i], a);
-            if (b) rr *= ipow(c[i], b);
-        }
-        tof += rf - rr;
-    }
-    return tof;
-}
-
-template <int NS>
-__global__ void __launch_bounds__(128) k_solve(NetView nv, CondView cv, const double* kf, const double* kr,
-                                               int64_t ld_k, SolveArgs a) {
-    extern __shared__ double lds[];
-    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int G = a.G;
-    const int64_t c = gid / G;
-    const int q = (int)(gid % G);
-    const int R = nv.NRXN;
-    // DRC lanes: q = 0 base, q = 2j+1 -> k_j*(1+eps), q = 2j+2 -> k_j*(1-eps)
-    const bool drc = (G > 1);
-    const bool active = (c < cv.n) && (!drc || q <= 2 * R);
-    double* kfs = lds + threadIdx.x;
-    double* krs = lds + (size_t)R * blockDim.x + threadIdx.x;
-    double tof = 0.0;
-    int st = PCK_ST_OK;
-    if (active) {
-        int pj = -1;
-        double pfac = 1.0;
-        if (drc && q > 0) { pj = (q - 1) >> 1; pfac = (q & 1) ? 1.0 + a.eps : 1.0 - a.eps; }
-        Lane<NS> L; double T;
-        lane_setup<NS>(nv, cv, c, L, T, lds + threadIdx.x, blockDim.x);
-        load_keff(nv, cv, c, kf, kr, ld_k, kfs, krs, blockDim.x, pj, pfac);
-        double y[NS];
-#pragma unroll
-        for (int i = 0; i < NS; ++i) y[i] = cv.y0[i * cv.ld_y0 + c * cv.s_y0];
-        int ns = 0;
-        st = integrate<NS>(nv, L, kfs, krs, blockDim.x, y, a.t0, a.t_end, a.rtol, a.atol, a.max_steps, ns);
-        if (st == PCK_ST_OK && a.newton) st = newton<NS>(nv, L, kfs, krs, blockDim.x, y, a.newton_iters);
-        tof = lane_tof<NS>(nv, L, kfs, krs, blockDim.x, y);
-        if (!drc) {
-            bool fin = isfinite(tof);
-#pragma unroll
-            for (int i = 0; i < NS; ++i) fin = fin && isfinite(y[i]);
-            if (!fin && st == PCK_ST_OK) st = PCK_ST_NONFINITE;
-            if (a.y) {
-#pragma unroll
-                for (int i = 0; i < NS; ++i) a.y[i * a.ld_y + c] = y[i];
-            }
-            if (a.tof) {
-                // old_system.py:526-527
-                a.tof[c] = a.want_activity ? (log((hP * tof) / (kB * T)) * (Rgas * T)) * 1.0e-3 / eVtokJ : tof;
-            }
-            if (a.status) a.status[c] = st;
-            if (a.nsteps) a.nsteps[c] = ns;
-        }
-    }
-    if (drc) {
-        // wavefront-shuffle combine: every lane of a condition's group lives in
-        // the same wavefront (G divides 64)
-        const int lane = threadIdx.x & 63;
-        const int base = lane - q;
-        const double t0 = __shfl(tof, base, 64);
-        const double tm = __shfl(tof, lane + 1 < 64 ? lane + 1 : lane, 64);
-        const int s0 = __shfl(st, base, 64);
-        const int sm = __shfl(st, lane + 1 < 64 ? lane + 1 : lane, 64);
-        if (active && (q & 1)) {
-            const int j = (q - 1) >> 1;
-            a.xi[j * a.ld_xi + c] = (tof - tm) / (2.0 * a.eps * t0);   // old_system.py:508
-            // status of the group = worst member
-            if (a.status && (st | sm)) atomicMax(&a.status[c], st > sm ? st : sm);
-        }
-        if (active && q == 0) {
-            if (a.tof0) a.tof0[c] = tof;
-            if (a.status && s0) atomicMax(&a.status[c], s0);
-        }
-    }
-}
+#include "mk_solver.h"
 
 // ----------------------------------------------------------------------------
 // C-ABI
@@ -627,6 +180,23 @@ extern "C" int pck_network_create(const int32_t* ip, int64_t n_ip, const double*
     nv.rxd = Dp + doff[PCK_D_RX]; nv.S = Dp + doff[PCK_D_STOICH]; nv.dyn = Dp + doff[PCK_D_DYN];
     nv.C = Dp + doff[PCK_D_CONS];
     net->nv = nv;
+    // structural digest -> compiled-in plan (same bytes as network.py: structural_digest)
+    {
+        const int32_t hdr3[3] = {nv.NDYN, nv.NRXN, nv.NCONS};
+        unsigned long long h = 0xcbf29ce484222325ULL;
+        h = fnv1a(h, hdr3, sizeof(hdr3));
+        h = fnv1a(h, ip + oef, sizeof(int32_t) * nv.NRXN * nv.NDYN);
+        h = fnv1a(h, ip + oer, sizeof(int32_t) * nv.NRXN * nv.NDYN);
+        h = fnv1a(h, dp + doff[PCK_D_STOICH], sizeof(double) * nv.NDYN * nv.NRXN);
+        h = fnv1a(h, dp + doff[PCK_D_DYN], sizeof(double) * 4 * nv.NDYN);
+        h = fnv1a(h, dp + doff[PCK_D_CONS], sizeof(double) * nv.NCONS * nv.NDYN);
+        h = fnv1a(h, ip + ocp, sizeof(int32_t) * nv.NCONS);
+        net->digest = h;
+#define PCK_MATCH(id, T) \
+        if (h == T::DIGEST && nv.NDYN == T::NS && nv.NRXN == T::R && nv.NCONS == T::NCONS) net->spec = id;
+        PCK_COMPILED_NETWORKS(PCK_MATCH)
+#undef PCK_MATCH
+    }
     *out = net;
     return PCK_OK;
 }
@@ -643,6 +213,13 @@ extern "C" int pck_network_dims(const pck_network* net, int32_t* dims) {
     const NetView& v = net->nv;
     dims[0] = v.D; dims[1] = v.NTH; dims[2] = v.NREG; dims[3] = v.NRXN; dims[4] = v.NDYN;
     dims[5] = v.NFIX; dims[6] = v.NCONS; dims[7] = v.NTOF; dims[8] = v.nfeat;
+    dims[9] = net->spec;
+    return PCK_OK;
+}
+
+extern "C" int pck_network_set_plan_mode(pck_network* net, int force_runtime_plan) {
+    if (!net) return fail(PCK_E_ARG, "null network%s", "");
+    net->force_runtime_plan = force_runtime_plan ? 1 : 0;
     return PCK_OK;
 }
 
@@ -775,9 +352,17 @@ static int launch_solve(pck_network* net, const pck_conditions* cond, const pck_
     const int64_t lanes = n * a.G;
     const size_t shm = lds_bytes(R, net->nv.NDYN, B);
     dim3 g((unsigned)((lanes + B - 1) / B));
-#define CALL(N) hipLaunchKernelGGL(k_solve<N>, g, dim3(B), shm, s, net->nv, cview(cond), kf, kr, n, a)
-    PCK_NS_SWITCH(net->nv.NDYN, CALL)
+    if (net->spec && !net->force_runtime_plan) {
+#define PCK_LAUNCH_CT(id, T)                                                                           \
+        if (net->spec == id)                                                                          \
+            hipLaunchKernelGGL(k_solve<PlanCT<T>>, g, dim3(B), shm, s, net->nv, cview(cond), kf, kr, n, a);
+        PCK_COMPILED_NETWORKS(PCK_LAUNCH_CT)
+#undef PCK_LAUNCH_CT
+    } else {
+#define CALL(N) hipLaunchKernelGGL(k_solve<PlanRT<N>>, g, dim3(B), shm, s, net->nv, cview(cond), kf, kr, n, a)
+        PCK_NS_SWITCH(net->nv.NDYN, CALL)
 #undef CALL
+    }
     HIPCHK(hipGetLastError());
     return PCK_OK;
 }

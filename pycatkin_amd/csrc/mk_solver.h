@@ -1,0 +1,640 @@
+// Solver-side device code, templated on a network "plan policy":
+//
+//   PlanRT<NS>   reads the uploaded plan at run time (any network with NS <= 8);
+//                the reaction loop is a runtime loop over uniform plan data,
+//                k_eff lives in LDS.
+//   PlanCT<Net>  a network compiled in (networks.h, generated from the same
+//                plan by tools/gen_networks.py): every loop over reactions and
+//                species is unrolled against constexpr tables, zero
+//                stoichiometry / exponents vanish at compile time and k_eff
+//                lives in VGPRs.  Selected at pck_network_create by the plan's
+//                structural digest; results are identical to PlanRT.
+//
+// One lane = one condition (or one DRC perturbation of a condition).
+#pragma once
+#include "mk_device.h"
+#include "networks.h"
+
+namespace pck {
+
+template <int NS_>
+struct PlanRT {
+    static constexpr int NS = NS_;
+    static constexpr bool CT = false;
+    static constexpr int RMAX = 1;
+    const NetView& nv;
+    __device__ explicit PlanRT(const NetView& v) : nv(v) {}
+    __device__ int R() const { return nv.NRXN; }
+    __device__ int ef(int j, int i) const { return nv.expf[j * NS + i]; }
+    __device__ int er(int j, int i) const { return nv.expr[j * NS + i]; }
+    __device__ double S(int i, int j) const { return nv.S[i * nv.NRXN + j]; }
+    __device__ double cf(int i) const { return nv.dyn[4 * i + 0]; }
+    __device__ double rs0(int i) const { return nv.dyn[4 * i + 1]; }
+    __device__ double rsT(int i) const { return nv.dyn[4 * i + 2]; }
+    __device__ double fl(int i) const { return nv.dyn[4 * i + 3]; }
+    __device__ int ncons() const { return nv.NCONS; }
+    __device__ double C(int l, int i) const { return nv.C[l * NS + i]; }
+    __device__ int cpiv(int l) const { return nv.cpiv[l]; }
+};
+
+template <class Net>
+struct PlanCT {
+    static constexpr int NS = Net::NS;
+    static constexpr bool CT = true;
+    static constexpr int RMAX = Net::R;
+    const NetView& nv;
+    __device__ explicit PlanCT(const NetView& v) : nv(v) {}
+    __device__ static constexpr int R() { return Net::R; }
+    __device__ static constexpr int ef(int j, int i) { return Net::ef(j, i); }
+    __device__ static constexpr int er(int j, int i) { return Net::er(j, i); }
+    __device__ static constexpr double S(int i, int j) { return Net::S(i, j); }
+    __device__ static constexpr double cf(int i) { return Net::dyn(i, 0); }
+    __device__ static constexpr double rs0(int i) { return Net::dyn(i, 1); }
+    __device__ static constexpr double rsT(int i) { return Net::dyn(i, 2); }
+    __device__ static constexpr double fl(int i) { return Net::dyn(i, 3); }
+    __device__ static constexpr int ncons() { return Net::NCONS; }
+    __device__ static constexpr double C(int l, int i) { return Net::C(l, i); }
+    __device__ static constexpr int cpiv(int l) { return Net::cpiv(l); }
+};
+
+// k_eff storage: LDS columns (runtime plans) or registers (compiled plans)
+struct KLds {
+    double* kf;
+    double* kr;
+    int ks;
+    __device__ double f(int j) const { return kf[j * ks]; }
+    __device__ double r(int j) const { return kr[j * ks]; }
+    __device__ void set(int j, double a, double b) { kf[j * ks] = a; kr[j * ks] = b; }
+};
+template <int R>
+struct KReg {
+    double kf[R], kr[R];
+    __device__ double f(int j) const { return kf[j]; }
+    __device__ double r(int j) const { return kr[j]; }
+    __device__ void set(int j, double a, double b) { kf[j] = a; kr[j] = b; }
+};
+
+// loop over reactions: unrolled for compiled plans, runtime otherwise
+template <class P, class F>
+__device__ __forceinline__ void for_rxn(const P& p, F&& body) {
+    if constexpr (P::CT) {
+#pragma unroll
+        for (int j = 0; j < P::RMAX; ++j) body(j);
+    } else {
+        for (int j = 0; j < p.R(); ++j) body(j);
+    }
+}
+
+template <int NS>
+struct Lane {
+    double T;
+    const double* ins;   // this lane's inflow column in LDS (stride ks), flow rows only
+    int ks;
+};
+
+// ---------------------------------------------------------------------------
+// Species rates / Jacobian.  pycatkin/classes/old_system.py:202-313 with
+// reactor.py rhs/jacobian, and system.py:345-508 -- one mass-action form once
+// the host folds fixed species and weights into the plan:
+//   f_i = rs_i * sum_j S_ij (kf_j prod c^a - kr_j prod c^b) + fl_i (in_i - y_i),
+//   c_i = cf_i y_i,  rs_i = rs0_i + rsT_i T.
+// ---------------------------------------------------------------------------
+template <class P, class K>
+__device__ __forceinline__ void rhs(const P& p, const Lane<P::NS>& L, const K& k, const double (&y)[P::NS],
+                                    double (&f)[P::NS]) {
+    constexpr int NS = P::NS;
+    double c[NS];
+#pragma unroll
+    for (int i = 0; i < NS; ++i) { c[i] = p.cf(i) * y[i]; f[i] = 0.0; }
+    for_rxn(p, [&](int j) {
+        double rf = k.f(j), rr = k.r(j);
+#pragma unroll
+        for (int i = 0; i < NS; ++i) {
+            if (p.ef(j, i)) rf *= ipow(c[i], p.ef(j, i));
+            if (p.er(j, i)) rr *= ipow(c[i], p.er(j, i));
+        }
+        const double net = rf - rr;
+#pragma unroll
+        for (int i = 0; i < NS; ++i) {
+            const double s = p.S(i, j);
+            if (s != 0.0) f[i] += s * net;
+        }
+    });
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+        f[i] *= (p.rsT(i) != 0.0) ? p.rs0(i) + p.rsT(i) * L.T : p.rs0(i);
+        if (p.fl(i) != 0.0) f[i] += p.fl(i) * (L.ins[i * L.ks] - y[i]);
+    }
+}
+
+template <class P, class K>
+__device__ __forceinline__ void jac(const P& p, const Lane<P::NS>& L, const K& k, const double (&y)[P::NS],
+                                    double (&J)[P::NS][P::NS]) {
+    constexpr int NS = P::NS;
+    double c[NS];
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+        c[i] = p.cf(i) * y[i];
+#pragma unroll
+        for (int q = 0; q < NS; ++q) J[i][q] = 0.0;
+    }
+    for_rxn(p, [&](int j) {
+        const double kf = k.f(j), kr = k.r(j);
+        double d[NS];
+#pragma unroll
+        for (int q = 0; q < NS; ++q) {
+            double v = 0.0;
+            if (p.ef(j, q)) {
+                double t = kf * (double)p.ef(j, q) * p.cf(q) * ipow(c[q], p.ef(j, q) - 1);
+#pragma unroll
+                for (int i = 0; i < NS; ++i)
+                    if (i != q && p.ef(j, i)) t *= ipow(c[i], p.ef(j, i));
+                v += t;
+            }
+            if (p.er(j, q)) {
+                double t = kr * (double)p.er(j, q) * p.cf(q) * ipow(c[q], p.er(j, q) - 1);
+#pragma unroll
+                for (int i = 0; i < NS; ++i)
+                    if (i != q && p.er(j, i)) t *= ipow(c[i], p.er(j, i));
+                v -= t;
+            }
+            d[q] = v;
+        }
+#pragma unroll
+        for (int i = 0; i < NS; ++i) {
+            const double s = p.S(i, j);
+            if (s != 0.0) {
+#pragma unroll
+                for (int q = 0; q < NS; ++q) J[i][q] += s * d[q];
+            }
+        }
+    });
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+        const double rs = (p.rsT(i) != 0.0) ? p.rs0(i) + p.rsT(i) * L.T : p.rs0(i);
+#pragma unroll
+        for (int q = 0; q < NS; ++q) J[i][q] *= rs;
+        J[i][i] -= p.fl(i);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// per-lane setup: LDS per lane (stride = blockDim) = [kf_eff R][kr_eff R][inflow NS]
+// ---------------------------------------------------------------------------
+__host__ __device__ inline size_t lds_bytes(int R, int NS, int B) {
+    return sizeof(double) * (size_t)(2 * (R > 0 ? R : 1) + NS) * B;
+}
+
+template <class P>
+__device__ __forceinline__ void lane_setup(const P& p, const NetView& nv, const CondView& cv, int64_t c,
+                                           Lane<P::NS>& L, double* lds_lane, int ks) {
+    L.T = cv.T[c * cv.sT];           // reactor.py:34-41: CSTR row scaling is linear in T
+    L.ks = ks;
+    double* ins = lds_lane + (size_t)2 * nv.NRXN * ks;
+    L.ins = ins;
+#pragma unroll
+    for (int i = 0; i < P::NS; ++i)  // 1/residence_time on CSTR gas rows (reactor.py:154-156)
+        if (p.fl(i) != 0.0) ins[i * ks] = cv.inflow ? cv.inflow[i * cv.ld_in + c * cv.s_in] : 0.0;
+}
+
+// effective k (fixed species folded in, optional DRC perturbation)
+template <class P, class K>
+__device__ __forceinline__ void load_keff(const P& p, const NetView& nv, const CondView& cv, int64_t c,
+                                          const double* kf, const double* kr, int64_t ld_k, K& k, int pj,
+                                          double pfac) {
+    for_rxn(p, [&](int j) {
+        double a = kf[j * ld_k + c], b = kr[j * ld_k + c];
+        for (int q = 0; q < nv.NFIX; ++q) {
+            const int ea = nv.foldf[j * nv.NFIX + q], eb = nv.foldr[j * nv.NFIX + q];
+            if (ea | eb) {
+                const double x = cv.fixc[q * cv.ld_fix + c * cv.s_fix];
+                if (ea) a *= ipow(x, ea);
+                if (eb) b *= ipow(x, eb);
+            }
+        }
+        if (j == pj) { a *= pfac; b *= pfac; }   // old_system.py:504-506: kf + eps*kf, kr*(1 + eps)
+        k.set(j, a, b);
+    });
+}
+
+// ---------------------------------------------------------------------------
+// RODAS4 (Hairer & Wanner, stiffly accurate 4(3) Rosenbrock, L-stable),
+// autonomous form:  (I/(h g) - J) k_i = f(u_i) + sum_j C_ij k_j / h,
+// u_{i+1} = y + sum_j a_ij k_j,  y_new = u_5 + k5 + k6,  error = k6.
+// ---------------------------------------------------------------------------
+namespace rodas4 {
+constexpr double g = 0.25;
+constexpr double a21 = 1.544, a31 = 0.9466785280815826, a32 = 0.2557011698983284;
+constexpr double a41 = 3.314825187068521, a42 = 2.896124015972201, a43 = 0.9986419139977817;
+constexpr double a51 = 1.221224509226641, a52 = 6.019134481288629, a53 = 12.53708332932087,
+                 a54 = -0.6878860361058950;
+constexpr double C21 = -5.6688, C31 = -2.430093356833875, C32 = -0.2063599157091915;
+constexpr double C41 = -0.1073529058151375, C42 = -9.594562251023355, C43 = -20.47028614809616;
+constexpr double C51 = 7.496443313967647, C52 = -10.24680431464352, C53 = -33.99990352819905,
+                 C54 = 11.70890893206160;
+constexpr double C61 = 8.083246795921522, C62 = -7.981132988064893, C63 = -31.52159432874371,
+                 C64 = 16.31930543123136, C65 = -6.058818238834054;
+}  // namespace rodas4
+
+template <class P, class K>
+__device__ int integrate(const P& p, const Lane<P::NS>& L, const K& k, double (&y)[P::NS], double t0,
+                         double t_end, double rtol, double atol, int max_steps, int& nsteps) {
+    using namespace rodas4;
+    constexpr int NS = P::NS;
+    nsteps = 0;
+    const double span = t_end - t0;
+    if (!(span > 0.0)) return PCK_ST_OK;
+    double F0[NS];
+    rhs(p, L, k, y, F0);
+    double cons0[PCK_MAX_CONS];
+    for (int l = 0; l < p.ncons(); ++l) {
+        double s = 0.0;
+#pragma unroll
+        for (int i = 0; i < NS; ++i) s += p.C(l, i) * y[i];
+        cons0[l] = s;
+    }
+    // initial step (Hairer/Wanner heuristic, scipy's select_initial_step, order 4)
+    double h;
+    {
+        double d0 = 0.0, d1 = 0.0;
+#pragma unroll
+        for (int i = 0; i < NS; ++i) {
+            const double sc = atol + rtol * fabs(y[i]);
+            d0 += (y[i] / sc) * (y[i] / sc);
+            d1 += (F0[i] / sc) * (F0[i] / sc);
+        }
+        d0 = sqrt(d0 / NS); d1 = sqrt(d1 / NS);
+        double h0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : 0.01 * d0 / d1;
+        h0 = fmin(h0, span);
+        double y1[NS], F1[NS];
+#pragma unroll
+        for (int i = 0; i < NS; ++i) y1[i] = y[i] + h0 * F0[i];
+        rhs(p, L, k, y1, F1);
+        double d2 = 0.0;
+#pragma unroll
+        for (int i = 0; i < NS; ++i) {
+            const double sc = atol + rtol * fabs(y[i]);
+            const double q = (F1[i] - F0[i]) / sc;
+            d2 += q * q;
+        }
+        d2 = sqrt(d2 / NS) / h0;
+        const double h1 = (d1 <= 1e-15 && d2 <= 1e-15) ? fmax(1e-6, h0 * 1e-3) : pow(0.01 / fmax(d1, d2), 0.2);
+        h = fmin(fmin(100.0 * h0, h1), span);
+    }
+    double t = t0;
+    double W[NS][NS];
+    int piv[NS];
+    while (t < t_end) {
+        if (nsteps >= max_steps) return PCK_ST_MAXSTEPS;
+        ++nsteps;
+        bool last = false;
+        if (t + h >= t_end) { h = t_end - t; last = true; }
+        jac(p, L, k, y, W);                               // W = I/(h g) - J
+        const double ig = 1.0 / (h * g);
+#pragma unroll
+        for (int i = 0; i < NS; ++i) {
+#pragma unroll
+            for (int q = 0; q < NS; ++q) W[i][q] = -W[i][q];
+            W[i][i] += ig;
+        }
+        if (!lu<NS>(W, piv)) { h *= 0.25; continue; }
+        const double ih = 1.0 / h;
+        double k1[NS], k2[NS], k3[NS], k4[NS], k5[NS], u[NS], fu[NS];
+#pragma unroll
+        for (int i = 0; i < NS; ++i) k1[i] = F0[i];
+        lu_solve<NS>(W, piv, k1);
+#pragma unroll
+        for (int i = 0; i < NS; ++i) u[i] = y[i] + a21 * k1[i];
+        rhs(p, L, k, u, fu);
+#pragma unroll
+        for (int i = 0; i < NS; ++i) k2[i] = fu[i] + ih * (C21 * k1[i]);
+        lu_solve<NS>(W, piv, k2);
+#pragma unroll
+        for (int i = 0; i < NS; ++i) u[i] = y[i] + a31 * k1[i] + a32 * k2[i];
+        rhs(p, L, k, u, fu);
+#pragma unroll
+        for (int i = 0; i < NS; ++i) k3[i] = fu[i] + ih * (C31 * k1[i] + C32 * k2[i]);
+        lu_solve<NS>(W, piv, k3);
+#pragma unroll
+        for (int i = 0; i < NS; ++i) u[i] = y[i] + a41 * k1[i] + a42 * k2[i] + a43 * k3[i];
+        rhs(p, L, k, u, fu);
+#pragma unroll
+        for (int i = 0; i < NS; ++i) k4[i] = fu[i] + ih * (C41 * k1[i] + C42 * k2[i] + C43 * k3[i]);
+        lu_solve<NS>(W, piv, k4);
+#pragma unroll
+        for (int i = 0; i < NS; ++i) u[i] = y[i] + a51 * k1[i] + a52 * k2[i] + a53 * k3[i] + a54 * k4[i];
+        rhs(p, L, k, u, fu);
+#pragma unroll
+        for (int i = 0; i < NS; ++i) k5[i] = fu[i] + ih * (C51 * k1[i] + C52 * k2[i] + C53 * k3[i] + C54 * k4[i]);
+        lu_solve<NS>(W, piv, k5);
+#pragma unroll
+        for (int i = 0; i < NS; ++i) u[i] += k5[i];
+        rhs(p, L, k, u, fu);
+        // k6 reuses k5's registers once k5 is folded into u
+#pragma unroll
+        for (int i = 0; i < NS; ++i)
+            k5[i] = fu[i] + ih * (C61 * k1[i] + C62 * k2[i] + C63 * k3[i] + C64 * k4[i] + C65 * k5[i]);
+        lu_solve<NS>(W, piv, k5);
+        bool finite = true;
+        double s = 0.0;
+#pragma unroll
+        for (int i = 0; i < NS; ++i) {
+            u[i] += k5[i];
+            finite = finite && isfinite(u[i]) && isfinite(k5[i]);
+            const double sc = atol + rtol * fmax(fabs(y[i]), fabs(u[i]));
+            const double r = k5[i] / sc;
+            s += r * r;
+        }
+        const double en = finite ? sqrt(s / NS) : INFINITY;
+        if (en <= 1.0) {
+            t = last ? t_end : t + h;
+#pragma unroll
+            for (int i = 0; i < NS; ++i) y[i] = u[i];
+            // Rosenbrock stages keep linear invariants only up to the rounding of
+            // the stiff LU; rescale each non-negative site balance back onto its
+            // initial total (multiplicative, so tiny coverages keep their digits)
+            for (int l = 0; l < p.ncons(); ++l) {
+                double sm = 0.0;
+                bool pos = true;
+#pragma unroll
+                for (int i = 0; i < NS; ++i) {
+                    pos = pos && (p.C(l, i) >= 0.0);
+                    sm += p.C(l, i) * y[i];
+                }
+                if (pos && sm > 0.0) {
+                    const double fct = cons0[l] / sm;
+#pragma unroll
+                    for (int i = 0; i < NS; ++i)
+                        if (p.C(l, i) != 0.0) y[i] *= fct;
+                }
+            }
+            rhs(p, L, k, y, F0);
+            const double fac = (en > 0.0) ? 0.9 * rsqrt(sqrt(en)) : 6.0;   // 0.9 en^(-1/4)
+            h *= fmin(6.0, fmax(0.2, fac));
+        } else {
+            h *= finite ? fmax(0.2, 0.9 * rsqrt(sqrt(en))) : 0.25;
+        }
+        if (!(h > 1e-15 * fmax(fabs(t), 1e-300)) && t < t_end) return PCK_ST_STEPFAIL;
+    }
+    return PCK_ST_OK;
+}
+
+// Newton on f(y) = 0 with the plan's conservation laws replacing their pivot
+// rows (old_system.py:385-468 polishes with scipy least_squares; a regular
+// root it converges to is the same).  Rows are equilibrated; a multiplicity
+// estimate accelerates near-double roots; a root that stays linearly
+// convergent (a site-starved surface approached algebraically) or lands on a
+// negative component is not regular -> PCK_ST_NEWTON, transient state kept.
+template <class P, class K>
+__device__ int newton(const P& p, const Lane<P::NS>& L, const K& k, double (&y)[P::NS], int iters) {
+    constexpr int NS = P::NS;
+    double b[PCK_MAX_CONS];
+    for (int l = 0; l < p.ncons(); ++l) {
+        double s = 0.0;
+#pragma unroll
+        for (int i = 0; i < NS; ++i) s += p.C(l, i) * y[i];
+        b[l] = s;
+    }
+    double z[NS];
+#pragma unroll
+    for (int i = 0; i < NS; ++i) z[i] = y[i];
+    bool conv = false;
+    double prev = INFINITY, lastq = 1.0;
+    int linear = 0;
+    for (int it = 0; it < iters; ++it) {
+        double G[NS], J[NS][NS];
+        int piv[NS];
+        rhs(p, L, k, z, G);
+        jac(p, L, k, z, J);
+        for (int l = 0; l < p.ncons(); ++l) {
+            const int pv = p.cpiv(l);
+            double s = 0.0;
+#pragma unroll
+            for (int i = 0; i < NS; ++i) s += p.C(l, i) * z[i];
+#pragma unroll
+            for (int i = 0; i < NS; ++i) {
+                if (i == pv) {
+                    G[i] = s - b[l];
+#pragma unroll
+                    for (int q = 0; q < NS; ++q) J[i][q] = p.C(l, q);
+                }
+            }
+        }
+        // row equilibration: rate rows (|J| ~ k p, up to 1e9) and the O(1)
+        // conservation rows must carry comparable weight, or the LU's backward
+        // error (eps * max row norm) leaks into the site balance
+#pragma unroll
+        for (int i = 0; i < NS; ++i) {
+            double m = 0.0;
+#pragma unroll
+            for (int q = 0; q < NS; ++q) m = fmax(m, fabs(J[i][q]));
+            const double sc = (m > 0.0) ? 1.0 / m : 1.0;
+#pragma unroll
+            for (int q = 0; q < NS; ++q) J[i][q] *= sc;
+            G[i] = -G[i] * sc;
+        }
+        if (!lu<NS>(J, piv)) break;
+        lu_solve<NS>(J, piv, G);
+        double alpha = 1.0;
+        if (linear >= 2 && lastq < 0.9) {
+            alpha = fmin(4.0, 1.0 / (1.0 - lastq));
+#pragma unroll
+            for (int i = 0; i < NS; ++i)
+                if (G[i] < 0.0 && z[i] > 0.0) alpha = fmin(alpha, 0.9 * z[i] / -G[i]);
+            alpha = fmax(alpha, 1.0);
+        }
+        double rel = 0.0, zmax = 0.0;
+        bool finite = true;
+#pragma unroll
+        for (int i = 0; i < NS; ++i) {
+            G[i] *= alpha;
+            z[i] += G[i];
+            finite = finite && isfinite(z[i]);
+            zmax = fmax(zmax, fabs(z[i]));
+        }
+        if (!finite) break;
+        // components below 1e-12 of the largest are held to an absolute
+        // 1e-24 * zmax: their relative digits sit under the residual's rounding
+#pragma unroll
+        for (int i = 0; i < NS; ++i) rel = fmax(rel, fabs(G[i]) / fmax(fabs(z[i]), 1e-12 * zmax + 1e-300));
+        if (rel < 1e-12 || (it >= 2 && rel < 1e-7 && rel > 0.5 * prev)) { conv = true; break; }
+        lastq = rel / prev;
+        linear = (rel > 0.25 * prev) ? linear + 1 : 0;
+        if (linear >= 12) break;
+        prev = rel;
+    }
+    if (!conv) return PCK_ST_NEWTON;
+#pragma unroll
+    for (int i = 0; i < NS; ++i)
+        if (z[i] < 0.0) return PCK_ST_NEWTON;
+#pragma unroll
+    for (int i = 0; i < NS; ++i) y[i] = z[i];
+    return PCK_ST_OK;
+}
+
+template <class P, class K>
+__device__ __forceinline__ double lane_tof(const P& p, const NetView& nv, const K& k, const double (&y)[P::NS]) {
+    // old_system.py:482-488: sum of (r_fwd - r_rev) over tof_terms
+    constexpr int NS = P::NS;
+    double c[NS];
+#pragma unroll
+    for (int i = 0; i < NS; ++i) c[i] = p.cf(i) * y[i];
+    double tof = 0.0;
+    for (int t = 0; t < nv.NTOF; ++t) {
+        const int jt = nv.tof[t];
+        for_rxn(p, [&](int j) {
+            if (j != jt) return;
+            double rf = k.f(j), rr = k.r(j);
+#pragma unroll
+            for (int i = 0; i < NS; ++i) {
+                if (p.ef(j, i)) rf *= ipow(c[i], p.ef(j, i));
+                if (p.er(j, i)) rr *= ipow(c[i], p.er(j, i));
+            }
+            tof += rf - rr;
+        });
+    }
+    return tof;
+}
+
+// ---------------------------------------------------------------------------
+// evaluation kernels (runtime plans): pck_species_rates / pck_jacobian
+// ---------------------------------------------------------------------------
+template <int NS>
+__global__ void __launch_bounds__(128) k_species_rates(NetView nv, CondView cv, const double* kf, const double* kr,
+                                                       int64_t ld_k, const double* y, int64_t ld_y, double* dydt) {
+    extern __shared__ double lds[];
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= cv.n) return;
+    PlanRT<NS> p(nv);
+    KLds k{lds + threadIdx.x, lds + (size_t)nv.NRXN * blockDim.x + threadIdx.x, (int)blockDim.x};
+    Lane<NS> L;
+    lane_setup(p, nv, cv, c, L, lds + threadIdx.x, blockDim.x);
+    load_keff(p, nv, cv, c, kf, kr, ld_k, k, -1, 1.0);
+    double yy[NS], f[NS];
+#pragma unroll
+    for (int i = 0; i < NS; ++i) yy[i] = y[i * ld_y + c];
+    rhs(p, L, k, yy, f);
+#pragma unroll
+    for (int i = 0; i < NS; ++i) dydt[i * ld_y + c] = f[i];
+}
+
+template <int NS>
+__global__ void __launch_bounds__(128) k_jacobian(NetView nv, CondView cv, const double* kf, const double* kr,
+                                                  int64_t ld_k, const double* y, int64_t ld_y, double* jo) {
+    extern __shared__ double lds[];
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= cv.n) return;
+    PlanRT<NS> p(nv);
+    KLds k{lds + threadIdx.x, lds + (size_t)nv.NRXN * blockDim.x + threadIdx.x, (int)blockDim.x};
+    Lane<NS> L;
+    lane_setup(p, nv, cv, c, L, lds + threadIdx.x, blockDim.x);
+    load_keff(p, nv, cv, c, kf, kr, ld_k, k, -1, 1.0);
+    double yy[NS], J[NS][NS];
+#pragma unroll
+    for (int i = 0; i < NS; ++i) yy[i] = y[i * ld_y + c];
+    jac(p, L, k, yy, J);
+#pragma unroll
+    for (int i = 0; i < NS; ++i)
+#pragma unroll
+        for (int q = 0; q < NS; ++q) jo[(i * NS + q) * ld_y + c] = J[i][q];
+}
+
+// ---------------------------------------------------------------------------
+// kernel (3)+(4): solve (+ TOF / activity, + DRC combine by wavefront shuffles)
+// ---------------------------------------------------------------------------
+struct SolveArgs {
+    double t0, t_end, rtol, atol, eps;
+    int max_steps, newton, newton_iters, want_activity;
+    double* y; int64_t ld_y;
+    double* tof; int32_t* status; int32_t* nsteps;
+    double* xi; int64_t ld_xi; double* tof0;   // DRC mode
+    int G;                                     // lanes per condition (1, or DRC group size)
+};
+
+template <class P>
+struct KFor {
+    using type = KLds;
+};
+template <class Net>
+struct KFor<PlanCT<Net>> {
+    using type = KReg<Net::R>;
+};
+
+template <class P>
+__global__ void __launch_bounds__(128) k_solve(NetView nv, CondView cv, const double* kf, const double* kr,
+                                               int64_t ld_k, SolveArgs a) {
+    constexpr int NS = P::NS;
+    extern __shared__ double lds[];
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int G = a.G;
+    const int64_t c = gid / G;
+    const int q = (int)(gid % G);
+    const int R = nv.NRXN;
+    P p(nv);
+    // DRC lanes: q = 0 base, q = 2j+1 -> k_j*(1+eps), q = 2j+2 -> k_j*(1-eps)
+    const bool drc = (G > 1);
+    const bool active = (c < cv.n) && (!drc || q <= 2 * R);
+    typename KFor<P>::type k;
+    if constexpr (!P::CT) {
+        k.kf = lds + threadIdx.x;
+        k.kr = lds + (size_t)R * blockDim.x + threadIdx.x;
+        k.ks = blockDim.x;
+    }
+    double tof = 0.0;
+    int st = PCK_ST_OK;
+    double T = 0.0;
+    if (active) {
+        int pj = -1;
+        double pfac = 1.0;
+        if (drc && q > 0) { pj = (q - 1) >> 1; pfac = (q & 1) ? 1.0 + a.eps : 1.0 - a.eps; }
+        Lane<NS> L;
+        lane_setup(p, nv, cv, c, L, lds + threadIdx.x, blockDim.x);
+        T = L.T;
+        load_keff(p, nv, cv, c, kf, kr, ld_k, k, pj, pfac);
+        double y[NS];
+#pragma unroll
+        for (int i = 0; i < NS; ++i) y[i] = cv.y0[i * cv.ld_y0 + c * cv.s_y0];
+        int ns = 0;
+        st = integrate(p, L, k, y, a.t0, a.t_end, a.rtol, a.atol, a.max_steps, ns);
+        if (st == PCK_ST_OK && a.newton) st = newton(p, L, k, y, a.newton_iters);
+        tof = lane_tof(p, nv, k, y);
+        if (!drc) {
+            bool fin = isfinite(tof);
+#pragma unroll
+            for (int i = 0; i < NS; ++i) fin = fin && isfinite(y[i]);
+            if (!fin && st == PCK_ST_OK) st = PCK_ST_NONFINITE;
+            if (a.y) {
+#pragma unroll
+                for (int i = 0; i < NS; ++i) a.y[i * a.ld_y + c] = y[i];
+            }
+            if (a.tof) {
+                // old_system.py:526-527
+                a.tof[c] = a.want_activity ? (log((hP * tof) / (kB * T)) * (Rgas * T)) * 1.0e-3 / eVtokJ : tof;
+            }
+            if (a.status) a.status[c] = st;
+            if (a.nsteps) a.nsteps[c] = ns;
+        }
+    }
+    if (drc) {
+        // wavefront-shuffle combine: every lane of a condition's group lives in
+        // the same wavefront (G divides 64)
+        const int lane = threadIdx.x & 63;
+        const int base = lane - q;
+        const double t0 = __shfl(tof, base, 64);
+        const double tm = __shfl(tof, lane + 1 < 64 ? lane + 1 : lane, 64);
+        const int s0 = __shfl(st, base, 64);
+        const int sm = __shfl(st, lane + 1 < 64 ? lane + 1 : lane, 64);
+        if (active && (q & 1)) {
+            const int j = (q - 1) >> 1;
+            a.xi[j * a.ld_xi + c] = (tof - tm) / (2.0 * a.eps * t0);   // old_system.py:508
+            // status of the group = worst member
+            if (a.status && (st | sm)) atomicMax(&a.status[c], st > sm ? st : sm);
+        }
+        if (active && q == 0) {
+            if (a.tof0) a.tof0[c] = tof;
+            if (a.status && s0) atomicMax(&a.status[c], s0);
+        }
+    }
+}
+
+}  // namespace pck

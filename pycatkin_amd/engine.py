@@ -42,10 +42,14 @@ class DeviceNetwork:
         L.check(self.lib.pck_network_create(self._ip.ctypes.data_as(C.c_void_p), self._ip.size,
                                             self._dp.ctypes.data_as(C.c_void_p), self._dp.size, C.byref(h)))
         self.h = h
-        dims = (C.c_int32 * 9)()
+        dims = (C.c_int32 * 10)()
         L.check(self.lib.pck_network_dims(self.h, dims))
         (self.D, self.NTH, self.NREG, self.NRXN, self.NDYN, self.NFIX, self.NCONS, self.NTOF,
-         self.nfeat) = list(dims)
+         self.nfeat, self.compiled_plan) = list(dims)
+
+    def set_plan_mode(self, force_runtime_plan):
+        """A/B switch between the compiled-in and the runtime-plan solver."""
+        L.check(self.lib.pck_network_set_plan_mode(self.h, int(bool(force_runtime_plan))))
 
     @classmethod
     def from_plan(cls, plan):

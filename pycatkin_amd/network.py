@@ -72,6 +72,8 @@ def _rref_pivots(C, tol=1e-10):
         r += 1
     A = A[:r]
     A[np.abs(A) < tol] = 0.0
+    near = np.abs(A - np.round(A)) < 1e-9          # site balances are integer rows
+    A[near] = np.round(A[near])
     return A, piv
 
 
@@ -405,3 +407,26 @@ def compile_forms(forms, states, descriptors=None):
                np.zeros(0), np.zeros(0), np.zeros(0), np.zeros(0)]
     ip, dp = _blobs(len(prog['descriptors']), prog['NTH'], len(prog['regs']), 0, 0, 0, 0, iblocks, dblocks, 0)
     return ip, dp, [int(s[0]) for s in prog['slots']], prog['descriptors']
+
+
+def structural_digest(ip, dp):
+    """FNV-1a 64 of the solver-side structure of a plan (NS, R, NCONS,
+    exponents, stoichiometry, dynamic-row coefficients, conservation rows and
+    pivots) -- the key pck_network_create matches against the compiled-in
+    networks of csrc/networks.h (same byte order as mk_kernels.hip)."""
+    ip = np.asarray(ip, np.int32)
+    dp = np.asarray(dp, np.float64)
+    NS, R, NC = int(ip[L.I_NDYN]), int(ip[L.I_NRXN]), int(ip[L.I_NCONS])
+    parts = [np.array([NS, R, NC], np.int32),
+             ip[ip[L.I_OFF_EXPF]: ip[L.I_OFF_EXPF] + R * NS],
+             ip[ip[L.I_OFF_EXPR]: ip[L.I_OFF_EXPR] + R * NS],
+             dp[ip[L.I_HDR + L.D_STOICH]: ip[L.I_HDR + L.D_STOICH] + NS * R],
+             dp[ip[L.I_HDR + L.D_DYN]: ip[L.I_HDR + L.D_DYN] + NS * 4],
+             dp[ip[L.I_HDR + L.D_CONS]: ip[L.I_HDR + L.D_CONS] + NC * NS],
+             ip[ip[L.I_OFF_CPIV]: ip[L.I_OFF_CPIV] + NC]]
+    h = 0xcbf29ce484222325
+    for part in parts:
+        for byte in np.ascontiguousarray(part).tobytes():
+            h ^= byte
+            h = (h * 0x100000001b3) & 0xFFFFFFFFFFFFFFFF
+    return h

@@ -233,3 +233,24 @@ def test_bad_blob_is_rejected(P):
     from pycatkin_amd.engine import DeviceNetwork
     with pytest.raises(RuntimeError):
         DeviceNetwork(np.zeros(5, np.int32), np.zeros(1))
+
+
+def test_compiled_plan_matches_runtime_plan(P, inputs):
+    """k_solve<PlanCT<Volcano>> (networks.h) and k_solve<PlanRT<4>> agree."""
+    from pycatkin_amd.functions.volcano import set_volcano_energies
+    s = P.read_from_input_file(os.path.join(inputs, 'COOxVolcano', 'input.json'))
+    set_volcano_energies(s)
+    net = s.device(('CO_ox',))
+    assert net.compiled_plan == 1
+    rng = np.random.default_rng(2)
+    n = 4096
+    kw = dict(T=np.full(n, 600.0), desc={'ECO': rng.uniform(-2.5, 0.5, n), 'EO': rng.uniform(-2.5, 0.5, n)},
+              tof_terms=('CO_ox',), steady=True, activity=True)
+    a = s.solve_batch(**kw)
+    net.set_plan_mode(True)
+    b = s.solve_batch(**kw)
+    net.set_plan_mode(False)
+    assert np.array_equal(a['status'], b['status'])
+    ok = a['status'] == 0
+    np.testing.assert_allclose(a['tof'][ok], b['tof'][ok], rtol=1e-9)
+    np.testing.assert_allclose(a['y'][:, ok], b['y'][:, ok], rtol=1e-8, atol=1e-15)
