@@ -89,6 +89,26 @@ def log(msg):
     print('[bench] ' + msg, file=sys.stderr, flush=True)
 
 
+def profiled_traffic(kernel_name, grid):
+    """HBM bytes per launch of `kernel_name` from the newest committed rocprofv3
+    PMC summary (profiles/r*/*/summary.json, written by tools/pmc_summary.py from
+    a tools/profile.sh run of this bench at the same grid), or (None, None)."""
+    import glob
+    key = kernel_name.replace('PlanCT<', 'PlanCT<pck::nets::')
+    found = None
+    for f in sorted(glob.glob(os.path.join(ROOT, 'profiles', 'r*', '*', 'summary.json'))):
+        try:
+            s = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        for k, v in s.items():
+            short = k.replace('pck::', '').replace(' ', '')
+            if short == key.replace('pck::', '').replace(' ', '') and 'traffic_bytes' in v \
+                    and v.get('grid', grid) == grid:
+                found = (v['traffic_bytes'], os.path.relpath(f, ROOT))
+    return found or (None, None)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -115,6 +135,7 @@ def main():
     from pycatkin_amd import _lib as L
     from pycatkin_amd.engine import _ptr
     from pycatkin_amd.functions.volcano import set_volcano_energies
+    from pycatkin_amd.parallel import weak_grid_rows
 
     sim = P.read_from_input_file(os.path.join(ROOT, 'tests', 'golden', 'inputs', 'COOxVolcano', 'input.json'))
     set_volcano_energies(sim)
@@ -123,9 +144,8 @@ def main():
     net.set_plan_mode(args.runtime_plan)
     kernel_name = 'k_solve<PlanRT<4>>' if (args.runtime_plan or not net.compiled_plan) else 'k_solve<PlanCT<Volcano>>'
     G = args.grid
-    eco_all = np.linspace(-2.5, 0.5, G * world)
     eo = np.linspace(-2.5, 0.5, G)
-    eco_loc = eco_all[rank * G:(rank + 1) * G]
+    eco_loc = weak_grid_rows(G, rank, world)        # rank's rows of the (world*G) x G grid
     E1, E2 = np.meshgrid(eco_loc, eo, indexing='ij')
     n = E1.size
     T = float(sim.params['temperature'])
@@ -193,6 +213,9 @@ def main():
     lane_eff = float(ns.mean() / wave_max.mean())     # useful lane-steps / issued wave-steps
     fl = flops_per_step(plan) * steps_total
     achieved = fl / (k3_ms * 1e-3) / 1e12
+    # algorithmic HBM bytes of one k_solve launch: kf, kr in; y, activity, status, steps out
+    algo_bytes = n * (16 * net.NRXN + 8 * net.NDYN + 8 + 4 + 4)
+    traffic, traffic_src = profiled_traffic(kernel_name, G)
 
     if dist:
         tt = torch.tensor([elapsed], dtype=torch.float64, device='cuda')
@@ -227,7 +250,9 @@ def main():
                                    'rtol 1e-8 / atol 1e-10, Newton steady-state polish, activity' % (G, G),
                        'grid_per_gpu': [G, G], 'global_grid': [G * world, G], 'parallelism': 'dp%d' % world},
             'roofline': {'bound': 'valu_fp64', 'achieved': achieved, 'peak': FP64_VECTOR_PEAK_TFLOPS,
-                         'unit': 'TFLOP/s', 'frac': achieved / FP64_VECTOR_PEAK_TFLOPS, 'traffic': None,
+                         'unit': 'TFLOP/s', 'frac': achieved / FP64_VECTOR_PEAK_TFLOPS, 'traffic': traffic,
+                         'traffic_unit': 'bytes per launch (rocprofv3 PMC FETCH_SIZE x2 + WRITE_SIZE)',
+                         'traffic_source': traffic_src, 'algorithmic_bytes': algo_bytes,
                          'kernel': kernel_name, 'kernel_ms': k3_ms, 'rate_constants_ms': k1_ms,
                          'flops_per_launch': fl, 'flops_per_step': flops_per_step(plan),
                          'integrator_steps': steps_total, 'lane_efficiency': lane_eff},

@@ -304,9 +304,15 @@ class System:
         self.solution = np.stack([self._full(plan, plan.y0_default), self._full(plan, r['y'][:, 0])])
         return self.solution
 
-    def find_steady(self, store_steady=False, plot_comparison=False, path=None):
-        """old_system.py:385-468: steady state from the transient end (or from the
-        start state when no transient was run)."""
+    def find_steady(self, *args, **kw):
+        """old_system.py:385-468 find_steady(store_steady, plot_comparison, path) for
+        formulation 'classic'; system.py:566-639 find_steady(max_iters, y0, method)
+        -> SteadyStateResults for formulation 'patched'."""
+        if self.formulation == 'patched':
+            return self.find_steady_state(*args, **kw)
+        return self._find_steady_classic(*args, **kw)
+
+    def _find_steady_classic(self, store_steady=False, plot_comparison=False, path=None):
         plan = self.plan()
         if self.solution is not None:
             pos = {s: i for i, s in enumerate(plan.species)}
@@ -376,9 +382,16 @@ class System:
 
     # patched-API steady state (system.py:566-639)
     def find_steady_state(self, max_iters=30, y0=None, method=None):
+        """system.py:566-639.  The reference restarts scipy `root` from a random
+        guess until the surface rates vanish and the sites sum to one; here the
+        guess (y0, or the start state: deterministic) is first integrated to
+        params['times'][-1] (1e6 s when no times are set) so that Newton
+        starts in the basin of the stable root, then polished."""
         plan = self.plan()
         yd = plan.y0_default if y0 is None else np.asarray(y0, float)[len(plan.fix):]
+        times = self.params.get('times')
+        t_end = float(times[-1]) if times is not None and len(times) else 1.0e6
         r = self.solve_batch(T=[self.params['temperature']], y0=np.asarray(yd)[:, None],
-                             t0=0.0, t_end=0.0, steady=True)
+                             t0=0.0, t_end=t_end, steady=True, newton_iters=max(int(max_iters), 30))
         x = np.concatenate([plan.fix_default, r['y'][:, 0]])
         return SteadyStateResults(x, bool(r['status'][0] == 0))

@@ -18,7 +18,7 @@ def run(sim_system, steady_state_solve=False, plot_results=False, save_results=F
     """presets.py:16-28"""
     sim_system.solve_odes()
     if steady_state_solve:
-        sim_system.find_steady(store_steady=True)
+        sim_system._find_steady_classic(store_steady=True)
 
 
 def _net_rates(sim_system, plan, finals, T, p=None):

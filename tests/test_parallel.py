@@ -1,0 +1,66 @@
+"""Multi-rank sharding / gather of condition grids on CPU (gloo, world_size 2)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from pycatkin_amd.parallel import gather_shards, shard_bounds, weak_grid_rows
+
+
+def test_shard_bounds_cover_exactly():
+    for n in (0, 1, 7, 1024, 1048577):
+        for world in (1, 2, 3, 8):
+            b = [shard_bounds(n, r, world) for r in range(world)]
+            assert b[0][0] == 0 and b[-1][1] == n
+            assert all(b[i][1] == b[i + 1][0] for i in range(world - 1))
+            assert max(y - x for x, y in b) - min(y - x for x, y in b) <= 1
+
+
+def test_weak_grid_rows_partition_the_axis():
+    world, G = 4, 16
+    rows = np.concatenate([weak_grid_rows(G, r, world) for r in range(world)])
+    np.testing.assert_array_equal(rows, np.linspace(-2.5, 0.5, G * world))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, n_total, q):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    a, b = shard_bounds(n_total, rank, world)
+    # stand-in for the per-rank solve: a deterministic function of the global index
+    local = torch.arange(a, b, dtype=torch.float64) * 0.5 + 1.0
+    full = gather_shards(local, n_total, dist)
+    t = torch.tensor([float(b - a)])
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        q.put((full.numpy().tolist(), float(t)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('n_total', [10, 1001])
+def test_gather_world2_gloo(n_total):
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, n_total, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    full, tmax = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    np.testing.assert_allclose(full, np.arange(n_total) * 0.5 + 1.0)
+    assert tmax == max(b - a for a, b in (shard_bounds(n_total, r, 2) for r in range(2)))
