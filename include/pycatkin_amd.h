@@ -15,8 +15,8 @@
  * ctypes / FFI binding would call for the whole batch:
  *
  *   pck_rate_constants  <- Reaction.calc_rate_constants      pycatkin/classes/reaction.py:94
- *                          (+ State.calc_free_energy          pycatkin/classes/state.py:556,
- *                             ScalingState.calc_free_energy   state.py:708,
+ *                          (+ State.calc_free_energy          pycatkin/classes/state.py:367,
+ *                             ScalingState.calc_free_energy   state.py:519,
  *                             UserDefinedReaction.calc_reaction_energy reaction.py:222)
  *   pck_species_rates   <- System.species_odes + Reactor.rhs  pycatkin/classes/old_system.py:227,
  *                                                             pycatkin/classes/reactor.py:91,141
@@ -165,7 +165,7 @@ int pck_network_dims(const pck_network* net, int32_t* dims);
 int pck_network_set_plan_mode(pck_network* net, int force_runtime_plan);
 
 /* Energy-program registers (eV) per condition: out[r][ld_out], r < NREG.
- * Replaces State.get_free_energy (state.py:577) / Reaction.get_reaction_energy
+ * Replaces State.get_free_energy (state.py:388) / Reaction.get_reaction_energy
  * (reaction.py:171) / get_reaction_barriers (reaction.py:182) for a batch.
  * Networks with NDYN == 0 are accepted for this call and pck_rate_constants. */
 int pck_energies(const pck_network* net, const pck_conditions* cond, double* out, int64_t ld_out,

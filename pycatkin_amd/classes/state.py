@@ -15,7 +15,7 @@ from ..energy import LinearForm, as_form, feature_form
 
 
 class State:
-    """Mirror of pycatkin.classes.state.State (state.py:8-265)."""
+    """Mirror of pycatkin.classes.state.State (state.py:10-464)."""
 
     def __init__(self, state_type=None, name=None, path=None, vibs_path=None, sigma=None,
                  mass=None, inertia=None, gasdata=None, add_to_energy=None, path_to_pickle=None,
@@ -48,17 +48,17 @@ class State:
         self.i_freq = None
         self.shape = None
         self.atoms = None
-        if freq is not None:                       # state.py:249-253
+        if freq is not None:                       # state.py:59-63
             self.freq_source = 'inputfile'
             self.freq = np.array(sorted(freq, reverse=True), dtype=float)
             self.i_freq = np.array(sorted(i_freq or [], reverse=True), dtype=float)
         if self.state_type == 'gas':
             assert self.sigma is not None
-            if self.inertia is not None:          # state.py:257-264
+            if self.inertia is not None:          # state.py:67-75
                 self.inertia = np.array([i if i > 1.0e-12 else 0.0 for i in self.inertia])
                 self.shape = len([i for i in self.inertia if i > 0.0])
 
-    # -- input readers (state.py:266-400) ------------------------------------
+    # -- input readers (state.py:77-211) ------------------------------------
     def get_atoms(self):
         if isinstance(self.read_from_alternate, dict) and 'get_atoms' in self.read_from_alternate:
             self.atoms, self.mass, self.inertia = self.read_from_alternate['get_atoms']()
@@ -92,7 +92,7 @@ class State:
         if freq is not None:
             freq = list(freq)
             i_freq = list(i_freq or [])
-            if self.truncate_freq:                # state.py:373-392
+            if self.truncate_freq:                # state.py:183-205
                 floor = 12.4 * 1e-3 / (h * JtoeV)
                 freq = [floor if (f * h * JtoeV * 1e3) < 12.4 else f for f in freq]
                 n_dof = len(freq) + len(i_freq) - (3 if self.state_type == 'gas' else 0)
@@ -105,7 +105,7 @@ class State:
             self.i_freq = []
 
     def calc_electronic_energy(self, verbose=False):
-        """state.py:436-453"""
+        """state.py:247-264"""
         if self.Gelec is None:
             if self.energy_source == 'datafile':
                 with open(self.path) as fh:
@@ -123,7 +123,7 @@ class State:
             self.get_vibrations()
 
     def use_freq(self):
-        """Modes kept for ZPE / vibrational free energy (state.py:464-474)."""
+        """Modes kept for ZPE / vibrational free energy (state.py:275-285)."""
         self._ensure_vib()
         f = np.asarray(self.freq if self.freq is not None else np.zeros(0), dtype=float).ravel()
         if self.state_type == 'gas':
@@ -137,12 +137,12 @@ class State:
         return f[0:f.shape[0] - ntrunc]
 
     def calc_zpe(self, verbose=False):
-        """state.py:455-476"""
+        """state.py:266-287"""
         if self.Gzpe is None:
             self.Gzpe = 0.5 * h * float(np.sum(self.use_freq())) * JtoeV
 
     def rot_inertia(self):
-        """sqrt(prod of non-zero principal moments) in kg m^2 (state.py:539-547)."""
+        """sqrt(prod of non-zero principal moments) in kg m^2 (state.py:350-358)."""
         from ..constants.physical_constants import amuA2tokgm2
         I = np.asarray(self.inertia, dtype=float) * amuA2tokgm2
         if self.shape == 2:
@@ -192,7 +192,7 @@ class State:
         return g
 
     def free_form(self):
-        """state.py:556-575 as a LinearForm (eV)."""
+        """state.py:367-386 as a LinearForm (eV)."""
         add = self.add_to_energy or 0.0
         if self.Gfree is not None:
             return as_form(self.Gfree) + add
@@ -213,7 +213,7 @@ class State:
 
 
 class ScalingState(State):
-    """Mirror of pycatkin.classes.state.ScalingState (state.py:655-779)."""
+    """Mirror of pycatkin.classes.state.ScalingState (state.py:466-589)."""
 
     def __init__(self, state_type=None, name=None, path=None, vibs_path=None, sigma=None,
                  mass=None, inertia=None, gasdata=None, add_to_energy=None, path_to_pickle=None,
@@ -237,7 +237,7 @@ class ScalingState(State):
         return g[idx] if isinstance(g, (list, tuple, np.ndarray)) else g
 
     def elec_form(self):
-        """state.py:679-706 (a scalar gradient applies to every scaling reaction)."""
+        """state.py:490-517 (a scalar gradient applies to every scaling reaction)."""
         assert self.scaling_reactions is not None and self.scaling_coeffs is not None
         e = as_form(self.scaling_coeffs['intercept'])
         for idx, r in enumerate(self.scaling_reactions.values()):
@@ -249,7 +249,7 @@ class ScalingState(State):
         return e
 
     def free_form(self):
-        """state.py:708-754"""
+        """state.py:519-565"""
         if not self.use_descriptor_as_reactant:
             return super().free_form()
         g = as_form(0.0)

@@ -73,7 +73,7 @@ __device__ __forceinline__ double ipow(double c, int e) {
 
 // ---------------------------------------------------------------------------
 // Kernel-1 body: thermochemistry features -> energy program -> k (one lane)
-// State free energies: pycatkin/classes/state.py:455-584; rate constants:
+// State free energies: pycatkin/classes/state.py:266-386; rate constants:
 // pycatkin/classes/reaction.py:94-168, pycatkin/functions/rate_constants.py.
 // feat: this lane's feature column base; stride = lane stride of the scratch.
 // ---------------------------------------------------------------------------
@@ -100,13 +100,13 @@ __device__ inline void thermo_features(const NetView& nv, double T, double p,
                     sf += nu;
                     sl += log(1.0 - exp(-nu * hP / kT));
                 }
-                gv = (sf != 0.0) ? zpe + (kT * sl) * JtoeV : zpe;     // state.py:502-507
+                gv = (sf != 0.0) ? zpe + (kT * sl) * JtoeV : zpe;     // state.py:313-318
             }
         }
         if (kind & PCK_TH_GAS) {
-            const double m = mass * amutokg;                          // state.py:518-520
+            const double m = mass * amutokg;                          // state.py:329-331
             gt = (-kT * log((kT / p) * pow(2.0 * PI * m * kT / (hP * hP), 1.5))) * JtoeV;
-            if (shape == 2) {                                         // state.py:540-547
+            if (shape == 2) {                                         // state.py:351-358
                 gr = (-kT * log(8.0 * PI * PI * kT * rotI / (sigma * hP * hP))) * JtoeV;
             } else {
                 gr = (-kT * log((sqrt(PI) / sigma) * pow(8.0 * PI * PI * kT / (hP * hP), 1.5) * rotI)) * JtoeV;

@@ -1,7 +1,7 @@
 // HIP kernels + C-ABI entry points of pycatkin_amd (gfx950 / MI355X).
 //
 //   k_rate_constants   kernel (1): thermochemistry -> energy program -> kf/kr,
-//                      one lane per condition (reaction.py:94, state.py:556)
+//                      one lane per condition (reaction.py:94, state.py:367)
 //   k_species_rates    kernel (2): mass-action rates over the plan (old_system.py:227)
 //   k_jacobian         kernel (2'): analytic Jacobian (old_system.py:293)
 //   k_solve<NS>        kernel (3): Rosenbrock W-method to t_end + Newton steady-state

@@ -1,7 +1,7 @@
 """Symbolic energies: the host half of kernel (1).
 
 The reference evaluates free energies and reaction energies one condition at a
-time in Python floats (pycatkin/classes/state.py:436-584,
+time in Python floats (pycatkin/classes/state.py:247-386,
 pycatkin/classes/reaction.py:43-69/222-274).  Here the same formulas are run
 ONCE per network with `LinearForm`s instead of floats.  Every energy in the
 reference is affine in a small feature vector

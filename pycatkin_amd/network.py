@@ -129,6 +129,12 @@ def _rx_type(rxn, states_by_name, rate_model):
             return t, (kads_c, c0, e)
         t = L.RX_ADS_KEQ if typ == 'ADSORPTION' else L.RX_DES_KEQ
         return t, (kads_c, 0.0, 0.0)
+    # any other reac_type (e.g. 'scaling' in examples/COOxReactor/input_AuPd.json)
+    # takes the Arrhenius branch whenever dGa_fwd != 0 (reaction.py:121); with no
+    # barrier at all the reference raises, and so does this.
+    ga = rxn.energy_forms().get('dGa_fwd')
+    if typ != 'GHOST' and ga is not None and not (ga.is_constant() and float(ga) == 0.0):
+        return L.RX_ARRHENIUS, None
     raise RuntimeError('Reaction with id %s has invalid `reaction.reac_type`, must be one of `arrhenius`, '
                        '`adsorption`, `desorption`, `ghost`' % rxn.name)
 

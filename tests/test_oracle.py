@@ -131,3 +131,38 @@ def test_patched_model_runs(inputs):
         fd = (m.fun_ss(zp) - m.fun_ss(zm)) / (2 * eps)
         # central differences of rates that cancel to ~1e-4 of their terms
         np.testing.assert_allclose(J[:, k], fd, rtol=1e-3, atol=1e-6 * np.max(np.abs(J[:, k])))
+
+
+def test_cooxreactor_conversion_golden(inputs):
+    """test/test_3.py: COOxReactor (Pd111, CSTR, OUTCAR + log.vib inputs),
+    run_temperatures([523], steady_state_solve=True) -> CO conversion
+    51.143 % +- 1e-3.  The input selects ode_solver 'ode' (lsoda)."""
+    spec = O.load_spec(os.path.join(inputs, 'COOxReactor', 'input_Pd111.json'))
+    m = O.ClassicModel(spec, T=523.0)
+    yT, _ = m.solve_odes(method='LSODA')
+    ys = m.find_steady(yT.copy())
+    assert m.regular
+    pin = spec['system']['inflow_state']['CO']
+    xco = 100.0 * (1.0 - ys[m.idx['CO']] / pin)
+    assert abs(xco - 51.143) <= 1e-3
+
+
+def test_outcar_reader_matches_oracle(inputs):
+    """Product OUTCAR / log.vib readers (pycatkin_amd.functions.outcar, host
+    code) against the oracle's independent restatement of ase's vasp-out read."""
+    from pycatkin_amd.functions.outcar import read_frequencies, read_outcar
+    data = os.path.join(inputs, 'COOxReactor', 'data')
+    for d in sorted(os.listdir(data)):
+        a = read_outcar(os.path.join(data, d))
+        o = O._outcar_final(os.path.join(data, d))
+        assert a.energy == o['energy']
+        assert abs(a.total_mass() - o['mass']) <= 1e-9 * o['mass']
+        np.testing.assert_allclose(a.moments_of_inertia(), o['inertia'], rtol=1e-12, atol=1e-9)
+        f, fi = read_frequencies(os.path.join(data, d))
+        g, gi = O._read_logvib(os.path.join(data, d))
+        np.testing.assert_allclose(f, g, rtol=1e-15)
+        np.testing.assert_allclose(fi, gi, rtol=1e-15)
+    # linear gas molecules: one vanishing principal moment (state.py:96-101)
+    for d in ('CO', 'O2', 'CO2'):
+        I = read_outcar(os.path.join(data, d)).moments_of_inertia()
+        assert np.sum(I > 1e-12) == 2
