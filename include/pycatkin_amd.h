@@ -50,10 +50,15 @@ extern "C" {
 #define PCK_E_HIP (-2)      /* HIP runtime error */
 #define PCK_E_SIZE (-3)     /* network exceeds the compiled kernel limits */
 
-/* kernel limits (thread-per-condition solver, dense state in registers) */
-#define PCK_MAX_DYN 8       /* dynamic species per condition (solver kernels) */
+/* kernel limits.  Networks with up to PCK_MAX_DYN_LANE dynamic species run
+ * one condition per lane (state, Jacobian and LU in VGPRs); larger ones (up to
+ * PCK_MAX_DYN) run one condition per lane group of 16/32/64 lanes, one
+ * species row per lane (csrc/mk_group.h). */
+#define PCK_MAX_DYN 64      /* dynamic species per condition (solver kernels) */
+#define PCK_MAX_DYN_LANE 8  /* ... on the one-lane-per-condition path */
 #define PCK_MAX_DYN_PLAN 64 /* dynamic species a plan may hold (rate constants / energies) */
-#define PCK_MAX_RXN 64      /* active reactions */
+#define PCK_MAX_RXN 256     /* active reactions */
+#define PCK_MAX_EXP 255     /* stoichiometric exponent */
 #define PCK_MAX_CONS 4      /* conservation laws */
 #define PCK_MAX_TOF 16      /* TOF terms */
 
@@ -160,9 +165,14 @@ int pck_network_destroy(pck_network* net);
 /* Sizes of a created network: dims[0..9] = D, NTH, NREG, NRXN, NDYN, NFIX, NCONS, NTOF,
  * n_features, compiled-plan id (0 = runtime plan; see csrc/networks.h). */
 int pck_network_dims(const pck_network* net, int32_t* dims);
-/* 1: always run the runtime-plan solver even when a compiled-in plan matches
- * the network's structural digest (for A/B checks); 0: default. */
-int pck_network_set_plan_mode(pck_network* net, int force_runtime_plan);
+/* Solver selection (A/B checks): PCK_PLAN_AUTO (default: compiled-in plan when
+ * the structural digest matches, else the runtime plan, lane-group solver
+ * beyond the one-lane limits), PCK_PLAN_RUNTIME (never the compiled-in plan),
+ * PCK_PLAN_GROUP (always the lane-group solver). */
+#define PCK_PLAN_AUTO 0
+#define PCK_PLAN_RUNTIME 1
+#define PCK_PLAN_GROUP 2
+int pck_network_set_plan_mode(pck_network* net, int mode);
 
 /* Energy-program registers (eV) per condition: out[r][ld_out], r < NREG.
  * Replaces State.get_free_energy (state.py:388) / Reaction.get_reaction_energy

@@ -14,7 +14,9 @@
 #include <stdio.h>
 #include <string.h>
 #include <new>
+#include <vector>
 #include "mk_device.h"
+#include "mk_group.h"
 
 using namespace pck;
 
@@ -26,8 +28,13 @@ struct pck_network {
     int64_t scratch_cap = 0;
     double* kbuf = nullptr;         // kf/kr scratch for pck_solve/pck_drc
     int64_t kbuf_cap = 0;
+    double* drcbuf = nullptr;       // lane-group DRC: [2R+1][n] TOF + [2R+1][n] status
+    int64_t drcbuf_cap = 0;
+    int32_t* d_gi = nullptr;        // sparse plan for the lane-group solver (mk_group.h)
+    double* d_gd = nullptr;
+    GrpView gv;
     int spec = 0;                   // id of the compiled-in plan (networks.h) or 0
-    int force_runtime_plan = 0;     // pck_network_set_plan_mode(net, 1): always the runtime plan
+    int plan_mode = PCK_PLAN_AUTO;  // pck_network_set_plan_mode
     unsigned long long digest = 0;
 };
 
@@ -150,8 +157,11 @@ extern "C" int pck_network_create(const int32_t* ip, int64_t n_ip, const double*
             const int ri = ip[orx + 6 * j + k];
             if (ri >= nv.NREG) return fail(PCK_E_ARG, "reaction register index%s out of range (%lld)", "", j);
         }
-        for (int i = 0; i < nv.NDYN; ++i)
-            if (ip[oef + j * nv.NDYN + i] < 0 || ip[oer + j * nv.NDYN + i] < 0) return fail(PCK_E_ARG, "negative exponent%s", "");
+        for (int i = 0; i < nv.NDYN; ++i) {
+            const int ea = ip[oef + j * nv.NDYN + i], eb = ip[oer + j * nv.NDYN + i];
+            if (ea < 0 || eb < 0) return fail(PCK_E_ARG, "negative exponent%s", "");
+            if (ea > PCK_MAX_EXP || eb > PCK_MAX_EXP) return fail(PCK_E_SIZE, "exponent%s above %lld", "", PCK_MAX_EXP);
+        }
     }
     for (int l = 0; l < nv.NCONS; ++l)
         if (ip[ocp + l] < 0 || ip[ocp + l] >= nv.NDYN) return fail(PCK_E_ARG, "conservation pivot%s out of range (%lld)", "", l);
@@ -165,7 +175,7 @@ extern "C" int pck_network_create(const int32_t* ip, int64_t n_ip, const double*
     if (e == hipSuccess) e = hipMemcpy(net->d_ip, ip, sizeof(int32_t) * n_ip, hipMemcpyHostToDevice);
     if (e == hipSuccess && n_dp > 0) e = hipMemcpy(net->d_dp, dp, sizeof(double) * n_dp, hipMemcpyHostToDevice);
     if (e != hipSuccess) {
-        hipFree(net->d_ip); hipFree(net->d_dp); delete net;
+        (void)hipFree(net->d_ip); (void)hipFree(net->d_dp); delete net;
         return fail(PCK_E_HIP, "HIP error: %s (%lld)", hipGetErrorString(e), (long long)e);
     }
     const int32_t* I = net->d_ip;
@@ -180,6 +190,47 @@ extern "C" int pck_network_create(const int32_t* ip, int64_t n_ip, const double*
     nv.rxd = Dp + doff[PCK_D_RX]; nv.S = Dp + doff[PCK_D_STOICH]; nv.dyn = Dp + doff[PCK_D_DYN];
     nv.C = Dp + doff[PCK_D_CONS];
     net->nv = nv;
+    // sparse plan for the lane-group solver: participants of each reaction,
+    // CSR of the stoichiometry by species
+    {
+        const int R = nv.NRXN, NS = nv.NDYN;
+        const double* S = dp + doff[PCK_D_STOICH];
+        const double* dyn = dp + doff[PCK_D_DYN];
+        std::vector<int32_t> gi, rx_ptr(1, 0), rx_sp, rx_e, row_ptr(1, 0), row_rx;
+        std::vector<double> rx_cf, row_s;
+        for (int j = 0; j < R; ++j) {
+            for (int i = 0; i < NS; ++i) {
+                const int ea = ip[oef + j * NS + i], eb = ip[oer + j * NS + i];
+                if (ea | eb) { rx_sp.push_back(i); rx_e.push_back((ea << 8) | eb); rx_cf.push_back(dyn[4 * i]); }
+            }
+            rx_ptr.push_back((int32_t)rx_sp.size());
+        }
+        for (int i = 0; i < NS; ++i) {
+            for (int j = 0; j < R; ++j)
+                if (S[i * R + j] != 0.0) { row_rx.push_back(j); row_s.push_back(S[i * R + j]); }
+            row_ptr.push_back((int32_t)row_rx.size());
+        }
+        const size_t o_rxp = 0, o_sp = o_rxp + rx_ptr.size(), o_e = o_sp + rx_sp.size(),
+                     o_rp = o_e + rx_e.size(), o_rr = o_rp + row_ptr.size(), ni = o_rr + row_rx.size();
+        gi.reserve(ni);
+        for (auto* v : {&rx_ptr, &rx_sp, &rx_e, &row_ptr, &row_rx}) gi.insert(gi.end(), v->begin(), v->end());
+        std::vector<double> gd(rx_cf);
+        gd.insert(gd.end(), row_s.begin(), row_s.end());
+        e = hipMalloc(&net->d_gi, sizeof(int32_t) * (gi.size() + 1));
+        if (e == hipSuccess) e = hipMalloc(&net->d_gd, sizeof(double) * (gd.size() + 1));
+        if (e == hipSuccess) e = hipMemcpy(net->d_gi, gi.data(), sizeof(int32_t) * gi.size(), hipMemcpyHostToDevice);
+        if (e == hipSuccess && !gd.empty())
+            e = hipMemcpy(net->d_gd, gd.data(), sizeof(double) * gd.size(), hipMemcpyHostToDevice);
+        if (e != hipSuccess) {
+            (void)hipFree(net->d_ip); (void)hipFree(net->d_dp); (void)hipFree(net->d_gi); (void)hipFree(net->d_gd);
+            delete net;
+            return fail(PCK_E_HIP, "HIP error: %s (%lld)", hipGetErrorString(e), (long long)e);
+        }
+        GrpView& g = net->gv;
+        g.rx_ptr = net->d_gi + o_rxp; g.rx_sp = net->d_gi + o_sp; g.rx_e = net->d_gi + o_e;
+        g.row_ptr = net->d_gi + o_rp; g.row_rx = net->d_gi + o_rr;
+        g.rx_cf = net->d_gd; g.row_s = net->d_gd + rx_cf.size();
+    }
     // structural digest -> compiled-in plan (same bytes as network.py: structural_digest)
     {
         const int32_t hdr3[3] = {nv.NDYN, nv.NRXN, nv.NCONS};
@@ -203,7 +254,8 @@ extern "C" int pck_network_create(const int32_t* ip, int64_t n_ip, const double*
 
 extern "C" int pck_network_destroy(pck_network* net) {
     if (!net) return PCK_OK;
-    hipFree(net->d_ip); hipFree(net->d_dp); hipFree(net->scratch); hipFree(net->kbuf);
+    (void)hipFree(net->d_ip); (void)hipFree(net->d_dp); (void)hipFree(net->scratch); (void)hipFree(net->kbuf);
+    (void)hipFree(net->d_gi); (void)hipFree(net->d_gd); (void)hipFree(net->drcbuf);
     delete net;
     return PCK_OK;
 }
@@ -217,9 +269,10 @@ extern "C" int pck_network_dims(const pck_network* net, int32_t* dims) {
     return PCK_OK;
 }
 
-extern "C" int pck_network_set_plan_mode(pck_network* net, int force_runtime_plan) {
+extern "C" int pck_network_set_plan_mode(pck_network* net, int mode) {
     if (!net) return fail(PCK_E_ARG, "null network%s", "");
-    net->force_runtime_plan = force_runtime_plan ? 1 : 0;
+    if (mode < PCK_PLAN_AUTO || mode > PCK_PLAN_GROUP) return fail(PCK_E_ARG, "unknown plan mode%s %lld", "", mode);
+    net->plan_mode = mode;
     return PCK_OK;
 }
 
@@ -234,7 +287,7 @@ static int check_cond(const pck_network* net, const pck_conditions* c, bool need
 
 static int ensure(double** buf, int64_t* cap, int64_t need) {
     if (*cap >= need) return PCK_OK;
-    hipFree(*buf);
+    (void)hipFree(*buf);
     *buf = nullptr;
     *cap = 0;
     HIPCHK(hipMalloc(buf, sizeof(double) * (need > 0 ? need : 1)));
@@ -289,6 +342,35 @@ extern "C" int pck_rate_constants(const pck_network* net, const pck_conditions* 
     default: return fail(PCK_E_SIZE, "NDYN%s unsupported", "");     \
     }
 
+// Lane-group path (mk_group.h) for networks beyond the one-lane-per-condition
+// limits: more than PCK_MAX_DYN_LANE dynamic species, a k_eff block that does
+// not fit LDS at 128 lanes per block, or DRC needing more than 64 lanes.
+static bool use_group(const pck_network* net, int lanes_per_cond) {
+    const NetView& v = net->nv;
+    return net->plan_mode == PCK_PLAN_GROUP || v.NDYN > PCK_MAX_DYN_LANE || lds_bytes(v.NRXN, v.NDYN, 128) > 64 * 1024 ||
+           lanes_per_cond > 64;
+}
+static inline int grp_nsp(int NS) { return NS <= 16 ? 16 : NS <= 32 ? 32 : NS <= 48 ? 48 : 64; }
+static inline int grp_g(int NS) { return NS <= 16 ? 16 : NS <= 32 ? 32 : 64; }
+#define PCK_GRP_SWITCH(NS, CALL)          \
+    if ((NS) <= 16) { CALL(16, 16); }      \
+    else if ((NS) <= 32) { CALL(32, 32); } \
+    else if ((NS) <= 48) { CALL(48, 64); } \
+    else { CALL(64, 64); }
+
+static int launch_grp_rates(const pck_network* net, const pck_conditions* cond, const double* kf, const double* kr,
+                            int64_t ld_k, const double* y, int64_t ld_y, double* out, int jac, hipStream_t s) {
+    const int NS = net->nv.NDYN;
+    const int per = 64 / grp_g(NS);
+    dim3 g((unsigned)((cond->n + per - 1) / per));
+    const size_t shm = sizeof(double) * per * grp_lds_doubles(net->nv.NRXN, grp_nsp(NS));
+#define CALL(P, GG) hipLaunchKernelGGL((k_rates_grp<P, GG>), g, dim3(64), shm, s, net->nv, net->gv, cview(cond), kf, kr, ld_k, y, ld_y, out, jac)
+    PCK_GRP_SWITCH(NS, CALL)
+#undef CALL
+    HIPCHK(hipGetLastError());
+    return PCK_OK;
+}
+
 extern "C" int pck_species_rates(const pck_network* net, const pck_conditions* cond, const double* kf,
                                  const double* kr, int64_t ld_k, const double* y, int64_t ld_y, double* dydt,
                                  void* stream) {
@@ -297,6 +379,7 @@ extern "C" int pck_species_rates(const pck_network* net, const pck_conditions* c
     const int64_t n = cond->n;
     if (n == 0) return PCK_OK;
     if (!kf || !kr || !y || !dydt || ld_k < n || ld_y < n) return fail(PCK_E_ARG, "bad state/rate arrays%s", "");
+    if (use_group(net, 1)) return launch_grp_rates(net, cond, kf, kr, ld_k, y, ld_y, dydt, 0, (hipStream_t)stream);
     const int B = 128;
     const size_t shm = lds_bytes(net->nv.NRXN, net->nv.NDYN, B);
     dim3 g((unsigned)((n + B - 1) / B));
@@ -314,6 +397,7 @@ extern "C" int pck_jacobian(const pck_network* net, const pck_conditions* cond, 
     const int64_t n = cond->n;
     if (n == 0) return PCK_OK;
     if (!kf || !kr || !y || !jo || ld_k < n || ld_y < n) return fail(PCK_E_ARG, "bad state/rate arrays%s", "");
+    if (use_group(net, 1)) return launch_grp_rates(net, cond, kf, kr, ld_k, y, ld_y, jo, 1, (hipStream_t)stream);
     const int B = 128;
     const size_t shm = lds_bytes(net->nv.NRXN, net->nv.NDYN, B);
     dim3 g((unsigned)((n + B - 1) / B));
@@ -334,7 +418,7 @@ static int check_params(const pck_solve_params* prm) {
 }
 
 static int launch_solve(pck_network* net, const pck_conditions* cond, const pck_solve_params* prm, SolveArgs a,
-                        hipStream_t s) {
+                        hipStream_t s, int drc_groups = 0) {
     const int64_t n = cond->n;
     if (n == 0) return PCK_OK;
     if (!cond->y0) return fail(PCK_E_ARG, "initial state y0 required%s", "");
@@ -348,11 +432,39 @@ static int launch_solve(pck_network* net, const pck_conditions* cond, const pck_
     a.t0 = prm->t0; a.t_end = prm->t_end; a.rtol = prm->rtol; a.atol = prm->atol; a.eps = prm->drc_eps;
     a.max_steps = prm->max_steps; a.newton = prm->newton; a.newton_iters = prm->newton_iters;
     a.want_activity = prm->want_activity;
+    if (drc_groups || use_group(net, a.G)) {
+        GrpArgs ga;
+        ga.M = drc_groups ? drc_groups : 1;
+        ga.tofbuf = nullptr;
+        ga.stbuf = nullptr;
+        if (drc_groups) {
+            const int64_t m = (int64_t)drc_groups * n;
+            rc = ensure(&net->drcbuf, &net->drcbuf_cap, m + (m + 1) / 2);
+            if (rc) return rc;
+            ga.tofbuf = net->drcbuf;
+            ga.stbuf = (int32_t*)(net->drcbuf + m);
+        }
+        const int NS = net->nv.NDYN;
+        const int per = 64 / grp_g(NS);
+        const int64_t groups = n * ga.M;
+        dim3 g((unsigned)((groups + per - 1) / per));
+        const size_t shm = sizeof(double) * per * grp_lds_doubles(R, grp_nsp(NS));
+#define CALL(P, GG) hipLaunchKernelGGL((k_solve_grp<P, GG>), g, dim3(64), shm, s, net->nv, net->gv, cview(cond), kf, kr, n, a, ga)
+        PCK_GRP_SWITCH(NS, CALL)
+#undef CALL
+        HIPCHK(hipGetLastError());
+        if (drc_groups) {
+            hipLaunchKernelGGL(k_drc_combine, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, R, a.eps,
+                               ga.tofbuf, ga.stbuf, a.xi, a.ld_xi, a.tof0, a.status);
+            HIPCHK(hipGetLastError());
+        }
+        return PCK_OK;
+    }
     const int B = 128;
     const int64_t lanes = n * a.G;
     const size_t shm = lds_bytes(R, net->nv.NDYN, B);
     dim3 g((unsigned)((lanes + B - 1) / B));
-    if (net->spec && !net->force_runtime_plan) {
+    if (net->spec && net->plan_mode == PCK_PLAN_AUTO) {
 #define PCK_LAUNCH_CT(id, T)                                                                           \
         if (net->spec == id)                                                                          \
             hipLaunchKernelGGL(k_solve<PlanCT<T>>, g, dim3(B), shm, s, net->nv, cview(cond), kf, kr, n, a);
@@ -401,14 +513,16 @@ extern "C" int pck_drc(const pck_network* net, const pck_conditions* cond, const
     rc = check_params(prm);
     if (rc) return rc;
     const int R = net->nv.NRXN;
-    if (2 * R + 1 > 64) return fail(PCK_E_SIZE, "DRC needs 2R+1 <= 64 lanes%s (R=%lld)", "", R);
     if (!(prm->drc_eps > 0.0 && prm->drc_eps < 1.0)) return fail(PCK_E_ARG, "drc_eps must be in (0,1)%s", "");
     if (cond->n > 0 && (!xi || ld_xi < cond->n)) return fail(PCK_E_ARG, "bad xi output%s", "");
     int G = 1;
     while (G < 2 * R + 1) G <<= 1;
-    if (status && cond->n > 0) HIPCHK(hipMemsetAsync(status, 0, sizeof(int32_t) * cond->n, (hipStream_t)stream));
     SolveArgs a;
     memset(&a, 0, sizeof(a));
     a.xi = xi; a.ld_xi = ld_xi; a.tof0 = tof0; a.status = status; a.G = G;
-    return launch_solve(const_cast<pck_network*>(net), cond, prm, a, (hipStream_t)stream);
+    pck_network* nn = const_cast<pck_network*>(net);
+    // lane-group networks: one group per (condition, perturbation), combined after
+    if (use_group(net, G)) return launch_solve(nn, cond, prm, a, (hipStream_t)stream, 2 * R + 1);
+    if (status && cond->n > 0) HIPCHK(hipMemsetAsync(status, 0, sizeof(int32_t) * cond->n, (hipStream_t)stream));
+    return launch_solve(nn, cond, prm, a, (hipStream_t)stream);
 }

@@ -47,9 +47,10 @@ class DeviceNetwork:
         (self.D, self.NTH, self.NREG, self.NRXN, self.NDYN, self.NFIX, self.NCONS, self.NTOF,
          self.nfeat, self.compiled_plan) = list(dims)
 
-    def set_plan_mode(self, force_runtime_plan):
-        """A/B switch between the compiled-in and the runtime-plan solver."""
-        L.check(self.lib.pck_network_set_plan_mode(self.h, int(bool(force_runtime_plan))))
+    def set_plan_mode(self, mode):
+        """A/B switch: 0 / False = auto, 1 / True = runtime plan (never the
+        compiled-in one), 2 = lane-group solver."""
+        L.check(self.lib.pck_network_set_plan_mode(self.h, int(mode)))
 
     @classmethod
     def from_plan(cls, plan):

@@ -1,0 +1,179 @@
+"""Lane-group solver (csrc/mk_group.h): networks with more than 8 dynamic
+species, through the C-ABI, against the oracle and the reference's vectors.
+
+Tolerances as in test_gpu_parity.py: rates / Jacobians 1e-11 relative,
+steady-state coverages 1e-6 relative (1e-15 absolute floor)."""
+import copy
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import mk_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLD = json.load(open(os.path.join(HERE, 'golden', 'ref_vectors.json')))
+
+
+@pytest.fixture(scope='module')
+def P():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip('no HIP device')
+    import pycatkin_amd
+    return pycatkin_amd
+
+
+def close(a, b, rtol=1e-6, floor=1e-15):
+    a, b = np.asarray(a), np.asarray(b)
+    return np.all(np.abs(a - b) <= rtol * np.abs(b) + floor)
+
+
+def _volcano(P, inputs):
+    from pycatkin_amd.functions.volcano import set_volcano_energies
+    s = P.read_from_input_file(os.path.join(inputs, 'COOxVolcano', 'input.json'))
+    set_volcano_energies(s)
+    return s
+
+
+def test_group_solver_matches_lane_solver_on_volcano(P, inputs):
+    """The volcano network forced onto the lane-group solver (PCK_PLAN_GROUP)
+    against the one-lane-per-condition runtime-plan solver."""
+    s = _volcano(P, inputs)
+    net = s.device(('CO_ox',))
+    rng = np.random.default_rng(11)
+    n = 1024
+    kw = dict(T=np.full(n, 600.0), desc={'ECO': rng.uniform(-2.5, 0.5, n), 'EO': rng.uniform(-2.5, 0.5, n)},
+              tof_terms=('CO_ox',), steady=True, activity=True)
+    net.set_plan_mode(1)
+    a = s.solve_batch(**kw)
+    net.set_plan_mode(2)
+    b = s.solve_batch(**kw)
+    net.set_plan_mode(0)
+    assert np.all((b['status'] == 0) | (b['status'] == 4)), np.unique(b['status'])
+    assert np.mean(a['status'] != b['status']) < 0.05
+    ok = (a['status'] == 0) & (b['status'] == 0)
+    assert ok.sum() > 0.8 * n
+    same = np.isclose(b['tof'], a['tof'], rtol=1e-9, atol=0.0) | (b['tof'] == a['tof'])
+    bad = ok & ~same
+    if os.path.isdir('gpurun_out'):
+        json.dump(dict(idx=np.flatnonzero(bad).tolist(), st=[a['status'][bad].tolist(), b['status'][bad].tolist()],
+                       act=[a['tof'][bad].tolist(), b['tof'][bad].tolist()],
+                       y_lane=a['y'][:, bad].T.tolist(), y_grp=b['y'][:, bad].T.tolist(),
+                       ECO=kw['desc']['ECO'][bad].tolist(), EO=kw['desc']['EO'][bad].tolist()),
+                  open('gpurun_out/diag_group_volcano.json', 'w'))
+    # bistable points whose transient has not settled at t_end may polish to a
+    # different root under different rounding; everything else agrees
+    assert bad.sum() <= max(2, 0.005 * ok.sum()), np.flatnonzero(bad)
+    np.testing.assert_allclose(b['y'][:, ok & same], a['y'][:, ok & same], rtol=1e-8, atol=1e-15)
+    # transient only (no polish): same integrator, same steps up to rounding
+    kw['steady'] = False
+    net.set_plan_mode(1)
+    a = s.solve_batch(**kw)
+    net.set_plan_mode(2)
+    b = s.solve_batch(**kw)
+    net.set_plan_mode(0)
+    assert np.all(b['status'] == 0)
+    np.testing.assert_allclose(b['tof'], a['tof'], rtol=1e-6)
+
+
+def test_group_rates_jacobian_on_volcano(P, inputs):
+    s = _volcano(P, inputs)
+    plan = s.plan()
+    net = s.device()
+    rng = np.random.default_rng(4)
+    n = 200
+    d = {'ECO': rng.uniform(-2.5, 0.5, n), 'EO': rng.uniform(-2.5, 0.5, n)}
+    T = rng.uniform(450, 750, n)
+    y = rng.uniform(0, 1, (len(plan.dyn), n))
+    Tt, p, dd, fx, y0, inflow = s._inputs(net, plan, n, T, None, d, None, None, None)
+    kf, kr = net.rate_constants(n, Tt, p, dd)
+    out = {}
+    for mode in (1, 2):
+        net.set_plan_mode(mode)
+        out[mode] = (net.species_rates(n, Tt, p, y, kf, kr, dd, fx, inflow).cpu().numpy(),
+                     net.jacobian(n, Tt, p, y, kf, kr, dd, fx, inflow).cpu().numpy())
+    net.set_plan_mode(0)
+    np.testing.assert_allclose(out[2][0], out[1][0], rtol=1e-12, atol=1e-300)
+    np.testing.assert_allclose(out[2][1], out[1][1], rtol=1e-12, atol=1e-300)
+
+
+def _dmtm(P, inputs, mode='classic'):
+    return P.read_from_input_file(os.path.join(inputs, 'DMTM', 'input.json'), rate_model=mode)
+
+
+@pytest.mark.parametrize('mode', ['classic', 'patched'])
+def test_dmtm_rates_jacobian_vs_oracle(P, inputs, mode):
+    """11 dynamic species: pck_species_rates / pck_jacobian (lane groups of 16)
+    vs old_system species_odes / species_jacobian (oracle, pinned by the
+    reference's own species_odes vectors)."""
+    s = _dmtm(P, inputs, mode)
+    plan = s.plan()
+    net = s.device()
+    assert net.NDYN == 11
+    spec = O.load_spec(os.path.join(inputs, 'DMTM', 'input.json'))
+    rng = np.random.default_rng(8)
+    n = 24
+    T = np.linspace(350.0, 900.0, n)
+    y = rng.uniform(0, 1, (11, n))
+    Tt, p, d, fx, y0, inflow = s._inputs(net, plan, n, T, None, None, None, None, None)
+    kf, kr = net.rate_constants(n, Tt, p, d)
+    f = net.species_rates(n, Tt, p, y, kf, kr, d, fx, inflow).cpu().numpy()
+    J = net.jacobian(n, Tt, p, y, kf, kr, d, fx, inflow).cpu().numpy()
+    for c in range(n):
+        m = O.ClassicModel(spec, T=T[c], mode=mode)
+        full = m.y0.copy()
+        dyn = [m.idx[nm] for nm in plan.dyn]
+        full[dyn] = y[:, c]
+        np.testing.assert_allclose(f[:, c], m.rhs(full)[dyn], rtol=1e-11, atol=1e-300)
+        Jr = m.jac(full)[np.ix_(dyn, dyn)]
+        np.testing.assert_allclose(J[:, :, c], Jr, rtol=1e-11, atol=1e-12 * np.abs(Jr).max())
+
+
+def test_dmtm_steady_and_tof_vs_reference(P, inputs):
+    """examples/DMTM: transient to t = 1e12 s then Newton polish at 400 / 600 /
+    800 K.  Steady coverages vs the oracle's polished root (1e-6) and vs the
+    reference's find_steady output (least_squares, 1e-5 on coverages > 1e-6);
+    TOF(r5 + r9) vs the reference's run_and_return_tof."""
+    s = _dmtm(P, inputs)
+    g = GOLD['dmtm_classic']
+    T = np.array(g['temperatures'])
+    r = s.solve_batch(T=T, tof_terms=('r5', 'r9'), steady=True, rtol=1e-10, atol=1e-14)
+    assert np.all(r['status'] == 0), r['status']
+    plan = s.plan(('r5', 'r9'))
+    spec = O.load_spec(os.path.join(inputs, 'DMTM', 'input.json'))
+    for k, t in enumerate(T):
+        m = O.ClassicModel(spec, T=t)
+        yT, _ = m.solve_odes(rtol=1e-10, atol=1e-14)
+        ys = m.find_steady(yT)
+        assert m.regular
+        dyn = [m.idx[nm] for nm in plan.dyn]
+        assert close(r['y'][:, k], ys[dyn]), (t, r['y'][:, k], ys[dyn])
+        ref = np.array(g['y_steady'][k])[[g['snames'].index(nm) for nm in plan.dyn]]
+        big = ref > 1e-6
+        np.testing.assert_allclose(r['y'][big, k], ref[big], rtol=1e-5)
+        np.testing.assert_allclose(r['tof'][k], g['tof'][k], rtol=1e-4)
+
+
+def test_dmtm_drc_vs_reference(P, inputs):
+    """degree_of_rate_control(['r5', 'r9'], eps=5e-2) at 400 / 600 / 800 K
+    (test/test_1.py:421-432 pins r9 as rate-controlling at 400 K).  The group
+    path runs 2R+1 = 23 perturbed solves per condition and combines them."""
+    s = _dmtm(P, inputs)
+    g = GOLD['dmtm_classic']
+    T = np.array(g['temperatures'])
+    r = s.drc_batch(('r5', 'r9'), T=T, eps=5.0e-2, steady=True, rtol=1e-10, atol=1e-14)
+    assert np.all(r['status'] == 0), r['status']
+    xi = np.array([r[name] for name in g['reactions']])
+    assert g['reactions'][int(np.argmax(xi[:, 0]))] == 'r9'
+    spec = O.load_spec(os.path.join(inputs, 'DMTM', 'input.json'))
+    for k, t in enumerate(T):
+        m = O.ClassicModel(spec, T=t)
+        ref = m.drc(['r5', 'r9'], eps=5.0e-2, steady=True)
+        for j, name in enumerate(g['reactions']):
+            assert abs(xi[j, k] - ref[name]) <= 1e-6 * max(1.0, abs(ref[name])), (t, name, xi[j, k], ref[name])
+        # the reference's own (transient, rtol 1e-6) DRC
+        np.testing.assert_allclose(xi[:, k], g['drc'][k], atol=2e-3)
