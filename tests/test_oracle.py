@@ -118,7 +118,7 @@ def test_volcano_grid_vs_reference_code(inputs):
 def test_patched_model_runs(inputs):
     """system.py formulation on test/CH4_input.json (BASELINE configs[0])."""
     spec = O.load_spec(os.path.join(inputs, 'CH4', 'input.json'))
-    O.ch4_setup(spec, 1.5, 0.2)                                 # test/tests.py:206-210
+    O.ch4_setup(spec, 1.5, 0.2)                                 # test/tests.py:40-42
     m = O.PatchedModel(spec)
     assert len(m.groups) == 2 and m.ngas == 8
     z0 = np.random.default_rng(0).uniform(0.1, 1.0, len(m.y0) - m.ngas)
