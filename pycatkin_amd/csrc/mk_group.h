@@ -1,38 +1,53 @@
 // Lane-group solver: one condition per group of G = 16 / 32 / 64 lanes of a
-// wavefront, one species row per lane.  Used for networks with more than
-// PCK_MAX_DYN_LANE dynamic species (DMTM: 11, test/CH4_input.json: 16, the
-// 50-species synthetic network) and for networks whose reaction count does
-// not fit the one-lane-per-condition LDS budget.
+// wavefront.  Used for networks with more than PCK_MAX_DYN_LANE dynamic
+// species (DMTM: 11, test/CH4_input.json: 16, the 50-species synthetic
+// network) and for networks whose reaction count does not fit the
+// one-lane-per-condition LDS budget.
 //
-//   lane i of a group owns species i: y_i, every Rosenbrock stage entry,
-//   row i of the iteration matrix (NSP doubles in VGPRs, static indices).
-//   Rates are evaluated from the concentration vector the group keeps in
-//   LDS, over the sparse plan (participants of each reaction, CSR of S by
-//   species) -- pycatkin/classes/old_system.py:202-313, system.py:345-508.
-//   The Jacobian row is scattered into an LDS column block, then loaded into
-//   registers.  Dense LU with partial pivoting across the group: the pivot is
-//   an integer max-reduction (|a| as float bits, lane id in the low 6 bits),
-//   the pivot row is broadcast through LDS, every row lane eliminates its own
-//   row.  Triangular solves broadcast one entry per column by __shfl.
-//   Norms / step-size decisions are butterfly all-reductions, bitwise equal
-//   on every lane of the group, so control flow is group-uniform.
+//   * lane i of a group owns species i: y_i, every Rosenbrock stage entry and
+//     row i of the iteration matrix (NSP doubles in VGPRs, static indices);
+//   * rates and the Jacobian are evaluated lane-per-reaction (reactions gl,
+//     gl+G, ...: balanced whatever the species degrees) from the group's
+//     concentration vector in LDS, and scattered into the species rates /
+//     the [NS][NS] Jacobian block with LDS fp64 atomics
+//     (pycatkin/classes/old_system.py:202-313, system.py:345-508);
+//   * dense LU with partial pivoting across the group: the pivot is an integer
+//     max-reduction of |a| (float bits, lane id in the low 6 bits), the pivot
+//     row is broadcast through LDS, every free row eliminates its own entries.
+//     The column loop is rolled: each row rotates left by one column per
+//     step so the active column is always W[0] (code O(NSP), static
+//     indices); after NSP steps the row is back in place;
+//   * triangular solves: one broadcast per column (v_readlane on a full
+//     wavefront, __shfl on 16/32-lane groups);
+//   * norms / step-size decisions are butterfly all-reductions, bitwise equal
+//     on every lane, so control flow is group-uniform.
 //
-// LDS per group (doubles): kf[R] kr[R] | c[NSP] | pivot row[NSP] | J[NSP][NSP]
+// LDS per group (doubles): kf[R] kr[R] | c[NSP] | cf[NSP] | f[NSP] | pivot row[NSP] |
+// perm[NSP] (int) | J[NS][NS]
 #pragma once
 #include "mk_device.h"
 #include "mk_solver.h"
 
 namespace pck {
 
-// Sparse plan (built by pck_network_create from the dense blocks).
+#define PCK_GRP_MAX_PART 6   // dynamic participants (species with an exponent) per reaction
+#define PCK_GRP_MAX_STOICH 6 // dynamic species with S != 0 per reaction
+#define PCK_GRP_MAX_EXP 31
+
+// One reaction.  Participant k: 16-bit field of w (k < 4: w01 >> 16k, else
+// w2 >> 16(k-4)) = species | ef << 6 | er << 11.  Stoichiometric entry m:
+// species (sp01 >> 8m) & 63 for m < 4, (sp2 >> 8(m-4)) & 63 otherwise, value s[m].
+struct GrpRec {
+    int32_t r, np, ns, pad0;
+    uint32_t w0, w1, w2, pad1;
+    uint32_t sp0, sp1, sp2, pad2;
+    uint32_t pad3[4];
+    double s[PCK_GRP_MAX_STOICH];
+};
+static_assert(sizeof(GrpRec) == 112, "GrpRec layout");
+
 struct GrpView {
-    const int32_t* rx_ptr;   // NRXN+1: participants of reaction r
-    const int32_t* rx_sp;    // participant species
-    const int32_t* rx_e;     // (forward exponent << 8) | reverse exponent
-    const double* rx_cf;     // participant's concentration factor cf
-    const int32_t* row_ptr;  // NDYN+1: CSR of S by species
-    const int32_t* row_rx;   // reaction
-    const double* row_s;     // S[i][r]
+    const GrpRec* rx;        // NRXN records
 };
 
 __device__ __forceinline__ void wsync() {
@@ -64,6 +79,18 @@ __device__ __forceinline__ int gmaxi(int v) {
     for (int m = G / 2; m >= 1; m >>= 1) v = max(v, __shfl_xor(v, m, G));
     return v;
 }
+// broadcast lane `src` (group-uniform) of the group
+template <int G>
+__device__ __forceinline__ double gbcast(double v, int src) {
+    if constexpr (G == 64) {
+        const int s = __builtin_amdgcn_readfirstlane(src);
+        const int lo = __builtin_amdgcn_readlane(__double2loint(v), s);
+        const int hi = __builtin_amdgcn_readlane(__double2hiint(v), s);
+        return __hiloint2double(hi, lo);
+    } else {
+        return __shfl(v, src, G);
+    }
+}
 
 // Per-group context: LDS blocks and this lane's species row.
 template <int NSP>
@@ -72,86 +99,119 @@ struct Grp {
     bool row;                 // gl < NS
     double* kf; double* kr;   // effective rate constants (fixed species folded, DRC perturbation)
     double* c;                // concentrations c_q = cf_q y_q
+    double* cf;               // concentration factors
+    double* f;                // species-rate accumulator
     double* pb;               // pivot-row broadcast
-    double* J;                // Jacobian scatter block, column-major: J[q*NSP + i]
-    double cf, rs, fl, in;    // this row's concentration factor, row scale, flow, inflow
+    int* perm;                // perm[k] = lane whose row was the pivot of column k
+    double* J;                // Jacobian block, column-major: J[q*NS + i]
+    double cfi, rs, fl, in;   // this row's concentration factor, row scale, flow, inflow
 };
 
-__device__ __forceinline__ double rate_net(const GrpView& g, const double* kf, const double* kr, const double* c,
-                                           int r) {
-    double a = kf[r], b = kr[r];
-    const int p1 = g.rx_ptr[r + 1];
-    for (int p = g.rx_ptr[r]; p < p1; ++p) {
-        const double x = c[g.rx_sp[p]];
-        const int e = g.rx_e[p];
-        const int ef = e >> 8, er = e & 255;
+// register copy of a record's index words (no indexed arrays -> no scratch)
+struct RecV {
+    int r, np, ns;
+    uint64_t w01;
+    uint32_t w2;
+    uint64_t sp01;
+    uint32_t sp2;
+};
+__device__ __forceinline__ RecV load_rec(const GrpRec* p) {
+    const uint4 a = *reinterpret_cast<const uint4*>(p);
+    const uint4 b = *(reinterpret_cast<const uint4*>(p) + 1);
+    const uint4 c = *(reinterpret_cast<const uint4*>(p) + 2);
+    RecV v;
+    v.r = (int)a.x; v.np = (int)a.y; v.ns = (int)a.z;
+    v.w01 = ((uint64_t)b.y << 32) | b.x; v.w2 = b.z;
+    v.sp01 = ((uint64_t)c.y << 32) | c.x; v.sp2 = c.z;
+    return v;
+}
+__device__ __forceinline__ int part_field(const RecV& R, int k) {
+    const uint32_t f = (k < 4) ? (uint32_t)(R.w01 >> (16 * k)) : (R.w2 >> (16 * (k - 4)));
+    return (int)(f & 0xffffu);
+}
+__device__ __forceinline__ int stoich_species(const RecV& R, int m) {
+    const uint32_t f = (m < 4) ? (uint32_t)(R.sp01 >> (8 * m)) : (R.sp2 >> (8 * (m - 4)));
+    return (int)(f & 63u);
+}
+
+__device__ __forceinline__ double rec_rate(const RecV& R, const double* kf, const double* kr, const double* c) {
+    double a = kf[R.r], b = kr[R.r];
+    for (int k = 0; k < R.np; ++k) {
+        const int f = part_field(R, k);
+        const double x = c[f & 63];
+        const int ef = (f >> 6) & 31, er = f >> 11;
         if (ef) a *= ipow(x, ef);
         if (er) b *= ipow(x, er);
     }
     return a - b;
 }
 
-// d(net_r)/d(y_q) for participant slot p0 of reaction r
-__device__ __forceinline__ double drate_net(const GrpView& g, const double* kf, const double* kr, const double* c,
-                                            int r, int p0) {
-    const int e0 = g.rx_e[p0];
-    const int ef0 = e0 >> 8, er0 = e0 & 255;
-    const double x0 = c[g.rx_sp[p0]];
-    double a = ef0 ? kf[r] * (double)ef0 * ipow(x0, ef0 - 1) : 0.0;
-    double b = er0 ? kr[r] * (double)er0 * ipow(x0, er0 - 1) : 0.0;
-    const int p1 = g.rx_ptr[r + 1];
-    for (int p = g.rx_ptr[r]; p < p1; ++p) {
-        if (p == p0) continue;
-        const double x = c[g.rx_sp[p]];
-        const int e = g.rx_e[p];
-        const int ef = e >> 8, er = e & 255;
+// d(net_r)/d(c_q) for participant k0 of the record's reaction
+__device__ __forceinline__ double rec_drate(const RecV& R, const double* kf, const double* kr, const double* c,
+                                            int k0) {
+    const int f0 = part_field(R, k0);
+    const int ef0 = (f0 >> 6) & 31, er0 = f0 >> 11;
+    const double x0 = c[f0 & 63];
+    double a = ef0 ? kf[R.r] * (double)ef0 * ipow(x0, ef0 - 1) : 0.0;
+    double b = er0 ? kr[R.r] * (double)er0 * ipow(x0, er0 - 1) : 0.0;
+    for (int k = 0; k < R.np; ++k) {
+        if (k == k0) continue;
+        const int f = part_field(R, k);
+        const double x = c[f & 63];
+        const int ef = (f >> 6) & 31, er = f >> 11;
         if (ef) a *= ipow(x, ef);
         if (er) b *= ipow(x, er);
     }
-    return (a - b) * g.rx_cf[p0];
+    return a - b;
+}
+
+template <int NSP>
+__device__ __forceinline__ void put_c(const Grp<NSP>& x, double y) {
+    wsync();                                   // previous readers of c / f are done
+    if (x.row) { x.c[x.gl] = x.cfi * y; x.f[x.gl] = 0.0; }
+    wsync();
 }
 
 // f_i = rs_i * sum_r S_ir net_r + fl_i (in_i - y_i)   (row lanes; 0 elsewhere)
-template <int NSP>
+template <int NSP, int G>
 __device__ __forceinline__ double grp_rhs(const GrpView& g, const Grp<NSP>& x, double y) {
-    wsync();                                   // previous readers of c are done
-    if (x.row) x.c[x.gl] = x.cf * y;
-    wsync();
-    double f = 0.0;
-    if (x.row) {
-        const int e1 = g.row_ptr[x.gl + 1];
-        for (int e = g.row_ptr[x.gl]; e < e1; ++e) f += g.row_s[e] * rate_net(g, x.kf, x.kr, x.c, g.row_rx[e]);
-        f = f * x.rs + x.fl * (x.in - y);
+    put_c(x, y);
+    for (int j = x.gl; j < x.R; j += G) {
+        const GrpRec* p = g.rx + j;
+        const RecV R = load_rec(p);
+        const double net = rec_rate(R, x.kf, x.kr, x.c);
+        for (int m = 0; m < R.ns; ++m) atomicAdd(x.f + stoich_species(R, m), p->s[m] * net);
     }
-    return f;
+    wsync();
+    return x.row ? x.f[x.gl] * x.rs + x.fl * (x.in - y) : 0.0;
 }
 
 // W[q] = sgn * dF_i/dy_q + (q == i ? shift : 0), with dF/dy including the flow
-// diagonal (-fl_i).  The scatter block is read back and cleared.
-template <int NSP>
+// diagonal (-fl_i).  The block is read back and cleared.
+template <int NSP, int G>
 __device__ __forceinline__ void grp_jac(const GrpView& g, const Grp<NSP>& x, double y, double sgn, double shift,
                                         double (&W)[NSP]) {
-    wsync();
-    if (x.row) x.c[x.gl] = x.cf * y;
-    wsync();
-    if (x.row) {
-        const int e1 = g.row_ptr[x.gl + 1];
-        for (int e = g.row_ptr[x.gl]; e < e1; ++e) {
-            const int r = g.row_rx[e];
-            const double s = g.row_s[e];
-            const int p1 = g.rx_ptr[r + 1];
-            for (int p = g.rx_ptr[r]; p < p1; ++p) {
-                const double d = drate_net(g, x.kf, x.kr, x.c, r, p);
-                x.J[g.rx_sp[p] * NSP + x.gl] += s * d;
-            }
+    put_c(x, y);
+    const int NS = x.NS;
+    for (int j = x.gl; j < x.R; j += G) {
+        const GrpRec* p = g.rx + j;
+        const RecV R = load_rec(p);
+        for (int k = 0; k < R.np; ++k) {
+            const int q = part_field(R, k) & 63;
+            const double d = rec_drate(R, x.kf, x.kr, x.c, k) * x.cf[q];
+            for (int m = 0; m < R.ns; ++m) atomicAdd(x.J + q * NS + stoich_species(R, m), p->s[m] * d);
         }
     }
+    wsync();
     const double sc = sgn * x.rs;
     const double dg = shift - sgn * x.fl;
 #pragma unroll
     for (int q = 0; q < NSP; ++q) {
-        const double v = x.J[q * NSP + x.gl];
-        x.J[q * NSP + x.gl] = 0.0;
+        double v = 0.0;
+        if (q < NS && x.row) {
+            v = x.J[q * NS + x.gl];
+            x.J[q * NS + x.gl] = 0.0;
+        }
         W[q] = sc * v + (q == x.gl ? dg : 0.0);
     }
 }
@@ -167,58 +227,68 @@ struct Perm {
     __device__ __forceinline__ int get(int k) const { return (int)((w[k >> 2] >> (8 * (k & 3))) & 255u); }
 };
 
-// In-place LU of the group's rows with partial pivoting.  step = column at
-// which this lane's row became the pivot (NSP: padding lane).  Multipliers
-// stay in the eliminated rows' columns, the pivot row keeps U and stores
-// 1/U_kk in its pivot column.  Returns false on a zero / non-finite pivot.
+// LU factors of the group's rows: multipliers in the eliminated rows'
+// columns, U in the pivot rows with 1/U_kk in the pivot column; pk[k] = lane
+// of the pivot row of column k; step = column at which this row was pivot.
+template <int NSP>
+struct LU {
+    double W[NSP];
+    Perm<NSP> pk;
+    int step;
+};
+
 template <int NSP, int G>
-__device__ __forceinline__ bool grp_lu(const Grp<NSP>& x, double (&W)[NSP], Perm<NSP>& pk, int& step) {
+__device__ __forceinline__ bool grp_lu(const Grp<NSP>& x, LU<NSP>& F) {
     bool fre = x.row;
     bool ok = true;
-    step = NSP;
-#pragma unroll
-    for (int i = 0; i < (NSP + 3) / 4; ++i) pk.w[i] = 0u;
-    // single-exit loops with group-uniform guards, so the column index stays static
-#pragma unroll
+    F.step = NSP;
+#pragma unroll 1
     for (int k = 0; k < NSP; ++k) {
-        if (k < x.NS && ok) {
-            const float mag = (float)fabs(W[k]);
+        // W[j] holds column (k + j) mod NSP; columns < k sit at j >= NSP - k
+        if (k < x.NS) {
+            const float mag = (float)fabs(F.W[0]);
             int key = fre ? (int)((__float_as_uint(mag) & ~63u) | (uint32_t)x.gl) : -1;
             key = gmaxi<G>(key);
             const int p = key & 63;
             wsync();
             if (x.gl == p) {
+                x.pb[0] = F.W[0];
 #pragma unroll
-                for (int j = k; j < NSP; ++j) x.pb[j] = W[j];
+                for (int j = 1; j < NSP; ++j) x.pb[j] = (j < NSP - k) ? F.W[j] : 0.0;
+                x.perm[k] = p;
+                F.W[0] = 1.0 / F.W[0];
                 fre = false;
-                step = k;
+                F.step = k;
             }
             wsync();
-            pk.set(k, p);
-            const double piv = x.pb[k];
-            ok = key >= 0 && piv != 0.0 && isfinite(piv);
-            const double inv = 1.0 / piv;
-            if (fre && ok) {
-                const double l = W[k] * inv;
-                W[k] = l;
+            const double piv = x.pb[0];
+            ok = ok && key >= 0 && piv != 0.0 && isfinite(piv);
+            if (ok && fre) {
+                const double l = F.W[0] / piv;
+                F.W[0] = l;
 #pragma unroll
-                for (int j = k + 1; j < NSP; ++j) W[j] -= l * x.pb[j];
+                for (int j = 1; j < NSP; ++j) F.W[j] -= l * x.pb[j];
             }
-            if (x.gl == p) W[k] = inv;
         }
+        const double w0 = F.W[0];
+#pragma unroll
+        for (int j = 0; j < NSP - 1; ++j) F.W[j] = F.W[j + 1];
+        F.W[NSP - 1] = w0;
     }
+    wsync();
+#pragma unroll
+    for (int q = 0; q < NSP; ++q) F.pk.set(q, q < x.NS ? x.perm[q] : 0);
     return ok;
 }
 
-// Solve LU x = b for the group; b_i on lane i in, x_i on lane i out.
+// Solve (LU) x = b for the group; b_i on lane i in, x_i on lane i out.
 template <int NSP, int G>
-__device__ __forceinline__ double grp_solve(const Grp<NSP>& x, const double (&W)[NSP], const Perm<NSP>& pk,
-                                            int step, double b) {
+__device__ __forceinline__ double grp_solve(const Grp<NSP>& x, const LU<NSP>& F, double b) {
 #pragma unroll
     for (int k = 0; k < NSP; ++k) {
         if (k < x.NS) {
-            const double bk = __shfl(b, pk.get(k), G);
-            if (step > k) b -= W[k] * bk;
+            const double bk = gbcast<G>(b, F.pk.get(k));
+            if (F.step > k) b -= F.W[k] * bk;
         }
     }
     double out = 0.0;
@@ -226,35 +296,38 @@ __device__ __forceinline__ double grp_solve(const Grp<NSP>& x, const double (&W)
     for (int kk = 0; kk < NSP; ++kk) {
         const int k = NSP - 1 - kk;
         if (k < x.NS) {
-            const double xk = __shfl(b * W[k], pk.get(k), G);
-            if (step < k) b -= W[k] * xk;
+            const double xk = gbcast<G>(b * F.W[k], F.pk.get(k));
+            if (F.step < k) b -= F.W[k] * xk;
             if (x.gl == k) out = xk;
         }
     }
-    return out;
+    return x.row ? out : 0.0;
 }
 
 // ---------------------------------------------------------------------------
 // RODAS4 on the group (same scheme, controller and projection as mk_solver.h)
 // ---------------------------------------------------------------------------
 template <int NSP, int G>
-__device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& gv, const Grp<NSP>& x, double& y, double t0,
-                             double t_end, double rtol, double atol, int max_steps, int& nsteps) {
+__device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& gv, const Grp<NSP>& x, double& y,
+                                             double t0, double t_end, double rtol, double atol, int max_steps,
+                                             int& nsteps) {
     using namespace rodas4;
     const int NS = x.NS;
     const double invNS = 1.0 / NS;
     nsteps = 0;
     const double span = t_end - t0;
     if (!(span > 0.0)) return PCK_ST_OK;
-    double F0 = grp_rhs(gv, x, y);
+    double F0 = grp_rhs<NSP, G>(gv, x, y);
     double cons0[PCK_MAX_CONS];
     double ci[PCK_MAX_CONS];
     bool cpos[PCK_MAX_CONS];
 #pragma unroll
-    for (int l = 0; l < PCK_MAX_CONS; ++l) if (l < nv.NCONS) {
-        ci[l] = x.row ? nv.C[l * NS + x.gl] : 0.0;
-        cons0[l] = gsum<G>(ci[l] * y);
-        cpos[l] = gmin<G>(ci[l]) >= 0.0;
+    for (int l = 0; l < PCK_MAX_CONS; ++l) {
+        if (l < nv.NCONS) {
+            ci[l] = x.row ? nv.C[l * NS + x.gl] : 0.0;
+            cons0[l] = gsum<G>(ci[l] * y);
+            cpos[l] = gmin<G>(ci[l]) >= 0.0;
+        }
     }
     double h;
     {
@@ -263,39 +336,36 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
         const double d1 = sqrt(gsum<G>(x.row ? (F0 / sc) * (F0 / sc) : 0.0) * invNS);
         double h0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : 0.01 * d0 / d1;
         h0 = fmin(h0, span);
-        const double F1 = grp_rhs(gv, x, y + h0 * F0);
+        const double F1 = grp_rhs<NSP, G>(gv, x, y + h0 * F0);
         const double q = (F1 - F0) / sc;
         const double d2 = sqrt(gsum<G>(x.row ? q * q : 0.0) * invNS) / h0;
         const double h1 = (d1 <= 1e-15 && d2 <= 1e-15) ? fmax(1e-6, h0 * 1e-3) : pow(0.01 / fmax(d1, d2), 0.2);
         h = fmin(fmin(100.0 * h0, h1), span);
     }
     double t = t0;
-    double W[NSP];
-    Perm<NSP> pk;
-    int step;
+    LU<NSP> F;
     while (t < t_end) {
         if (nsteps >= max_steps) return PCK_ST_MAXSTEPS;
         ++nsteps;
         bool last = false;
         if (t + h >= t_end) { h = t_end - t; last = true; }
         const double ig = 1.0 / (h * g);
-        grp_jac(gv, x, y, -1.0, ig, W);                  // W = I/(h g) - J
-        if (!grp_lu<NSP, G>(x, W, pk, step)) { h *= 0.25; continue; }
+        grp_jac<NSP, G>(gv, x, y, -1.0, ig, F.W);        // W = I/(h g) - J
+        if (!grp_lu<NSP, G>(x, F)) { h *= 0.25; continue; }
         const double ih = 1.0 / h;
-        const double k1 = grp_solve<NSP, G>(x, W, pk, step, F0);
-        double fu = grp_rhs(gv, x, y + a21 * k1);
-        const double k2 = grp_solve<NSP, G>(x, W, pk, step, fu + ih * (C21 * k1));
-        fu = grp_rhs(gv, x, y + a31 * k1 + a32 * k2);
-        const double k3 = grp_solve<NSP, G>(x, W, pk, step, fu + ih * (C31 * k1 + C32 * k2));
-        fu = grp_rhs(gv, x, y + a41 * k1 + a42 * k2 + a43 * k3);
-        const double k4 = grp_solve<NSP, G>(x, W, pk, step, fu + ih * (C41 * k1 + C42 * k2 + C43 * k3));
+        const double k1 = grp_solve<NSP, G>(x, F, F0);
+        double fu = grp_rhs<NSP, G>(gv, x, y + a21 * k1);
+        const double k2 = grp_solve<NSP, G>(x, F, fu + ih * (C21 * k1));
+        fu = grp_rhs<NSP, G>(gv, x, y + a31 * k1 + a32 * k2);
+        const double k3 = grp_solve<NSP, G>(x, F, fu + ih * (C31 * k1 + C32 * k2));
+        fu = grp_rhs<NSP, G>(gv, x, y + a41 * k1 + a42 * k2 + a43 * k3);
+        const double k4 = grp_solve<NSP, G>(x, F, fu + ih * (C41 * k1 + C42 * k2 + C43 * k3));
         double u = y + a51 * k1 + a52 * k2 + a53 * k3 + a54 * k4;
-        fu = grp_rhs(gv, x, u);
-        const double k5 = grp_solve<NSP, G>(x, W, pk, step, fu + ih * (C51 * k1 + C52 * k2 + C53 * k3 + C54 * k4));
+        fu = grp_rhs<NSP, G>(gv, x, u);
+        const double k5 = grp_solve<NSP, G>(x, F, fu + ih * (C51 * k1 + C52 * k2 + C53 * k3 + C54 * k4));
         u += k5;
-        fu = grp_rhs(gv, x, u);
-        const double k6 =
-            grp_solve<NSP, G>(x, W, pk, step, fu + ih * (C61 * k1 + C62 * k2 + C63 * k3 + C64 * k4 + C65 * k5));
+        fu = grp_rhs<NSP, G>(gv, x, u);
+        const double k6 = grp_solve<NSP, G>(x, F, fu + ih * (C61 * k1 + C62 * k2 + C63 * k3 + C64 * k4 + C65 * k5));
         u += k6;
         const bool fin_l = !x.row || (isfinite(u) && isfinite(k6));
         const double fin = gmin<G>(fin_l ? 1.0 : 0.0);
@@ -306,15 +376,17 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
         if (en <= 1.0) {
             t = last ? t_end : t + h;
             y = x.row ? u : 0.0;
-        #pragma unroll
-    for (int l = 0; l < PCK_MAX_CONS; ++l) if (l < nv.NCONS) {
-                const double sm = gsum<G>(ci[l] * y);
-                if (cpos[l] && sm > 0.0) {
-                    const double fct = cons0[l] / sm;
-                    if (ci[l] != 0.0) y *= fct;
+#pragma unroll
+            for (int l = 0; l < PCK_MAX_CONS; ++l) {
+                if (l < nv.NCONS) {
+                    const double sm = gsum<G>(ci[l] * y);
+                    if (cpos[l] && sm > 0.0) {
+                        const double fct = cons0[l] / sm;
+                        if (ci[l] != 0.0) y *= fct;
+                    }
                 }
             }
-            F0 = grp_rhs(gv, x, y);
+            F0 = grp_rhs<NSP, G>(gv, x, y);
             const double fac = (en > 0.0) ? 0.9 * rsqrt(sqrt(en)) : 6.0;
             h *= fmin(6.0, fmax(0.2, fac));
         } else {
@@ -327,44 +399,48 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
 
 // Newton steady-state polish (same rules as mk_solver.h: newton)
 template <int NSP, int G>
-__device__ __forceinline__ int grp_newton(const NetView& nv, const GrpView& g, const Grp<NSP>& x, double& y, int iters) {
+__device__ __forceinline__ int grp_newton(const NetView& nv, const GrpView& gv, const Grp<NSP>& x, double& y,
+                                          int iters) {
     const int NS = x.NS;
     double b[PCK_MAX_CONS], ci[PCK_MAX_CONS];
     int piv_l[PCK_MAX_CONS];
 #pragma unroll
-    for (int l = 0; l < PCK_MAX_CONS; ++l) if (l < nv.NCONS) {
-        ci[l] = x.row ? nv.C[l * NS + x.gl] : 0.0;
-        b[l] = gsum<G>(ci[l] * y);
-        piv_l[l] = nv.cpiv[l];
+    for (int l = 0; l < PCK_MAX_CONS; ++l) {
+        if (l < nv.NCONS) {
+            ci[l] = x.row ? nv.C[l * NS + x.gl] : 0.0;
+            b[l] = gsum<G>(ci[l] * y);
+            piv_l[l] = nv.cpiv[l];
+        }
     }
     double z = y;
     bool conv = false;
     double prev = INFINITY, lastq = 1.0;
     int linear = 0;
-    double W[NSP];
-    Perm<NSP> pk;
-    int step;
+    LU<NSP> F;
     for (int it = 0; it < iters; ++it) {
-        double Gv = grp_rhs(g, x, z);
-        grp_jac(g, x, z, 1.0, 0.0, W);
-    #pragma unroll
-    for (int l = 0; l < PCK_MAX_CONS; ++l) if (l < nv.NCONS) {
-            const double s = gsum<G>(ci[l] * z);
-            if (x.gl == piv_l[l]) {
-                Gv = s - b[l];
+        double Gv = grp_rhs<NSP, G>(gv, x, z);
+        grp_jac<NSP, G>(gv, x, z, 1.0, 0.0, F.W);
 #pragma unroll
-                for (int q = 0; q < NSP; ++q) W[q] = (q < NS) ? nv.C[l * NS + q] : 0.0;
+        for (int l = 0; l < PCK_MAX_CONS; ++l) {
+            if (l < nv.NCONS) {
+                const double s = gsum<G>(ci[l] * z);
+                if (x.gl == piv_l[l]) {
+                    Gv = s - b[l];
+#pragma unroll
+                    for (int q = 0; q < NSP; ++q) F.W[q] = (q < NS) ? nv.C[l * NS + q] : 0.0;
+                }
             }
         }
+        // row equilibration (rate rows up to 1e9, conservation rows O(1))
         double m = 0.0;
 #pragma unroll
-        for (int q = 0; q < NSP; ++q) m = fmax(m, fabs(W[q]));
+        for (int q = 0; q < NSP; ++q) m = fmax(m, fabs(F.W[q]));
         const double sc = (m > 0.0) ? 1.0 / m : 1.0;
 #pragma unroll
-        for (int q = 0; q < NSP; ++q) W[q] *= sc;
+        for (int q = 0; q < NSP; ++q) F.W[q] *= sc;
         Gv = -Gv * sc;
-        if (!grp_lu<NSP, G>(x, W, pk, step)) break;
-        double dz = grp_solve<NSP, G>(x, W, pk, step, Gv);
+        if (!grp_lu<NSP, G>(x, F)) break;
+        double dz = grp_solve<NSP, G>(x, F, Gv);
         double alpha = 1.0;
         if (linear >= 2 && lastq < 0.9) {
             alpha = fmin(4.0, 1.0 / (1.0 - lastq));
@@ -392,8 +468,8 @@ __device__ __forceinline__ int grp_newton(const NetView& nv, const GrpView& g, c
 // ---------------------------------------------------------------------------
 // group setup + kernels
 // ---------------------------------------------------------------------------
-__host__ __device__ inline size_t grp_lds_doubles(int R, int NSP) {
-    return (size_t)2 * (R > 0 ? R : 1) + 2 * (size_t)NSP + (size_t)NSP * NSP;
+__host__ __device__ inline size_t grp_lds_doubles(int R, int NSP, int NS) {
+    return (size_t)2 * (R > 0 ? R : 1) + 4 * (size_t)NSP + (size_t)(NSP + 1) / 2 + (size_t)NS * NS;
 }
 
 template <int NSP, int G>
@@ -408,8 +484,11 @@ __device__ __forceinline__ void grp_setup(const NetView& nv, const CondView& cv,
     x.kf = base;
     x.kr = base + (R > 0 ? R : 1);
     x.c = x.kr + (R > 0 ? R : 1);
-    x.pb = x.c + NSP;
-    x.J = x.pb + NSP;
+    x.cf = x.c + NSP;
+    x.f = x.cf + NSP;
+    x.pb = x.f + NSP;
+    x.perm = (int*)(x.pb + NSP);
+    x.J = x.pb + NSP + (NSP + 1) / 2;
     T = cv.T[c * cv.sT];
     for (int j = x.gl; j < R; j += G) {
         double a = kf[j * ld_k + c], b = kr[j * ld_k + c];
@@ -425,15 +504,16 @@ __device__ __forceinline__ void grp_setup(const NetView& nv, const CondView& cv,
         x.kf[j] = a;
         x.kr[j] = b;
     }
-#pragma unroll
-    for (int q = 0; q < NSP; ++q) x.J[q * NSP + x.gl] = 0.0;
-    x.cf = x.rs = x.fl = x.in = 0.0;
+    for (int q = 0; q < x.NS; ++q)
+        if (x.row) x.J[q * x.NS + x.gl] = 0.0;
+    x.cfi = x.rs = x.fl = x.in = 0.0;
     if (x.row) {
         const double* d = nv.dyn + 4 * x.gl;
-        x.cf = d[0];
+        x.cfi = d[0];
         x.rs = (d[2] != 0.0) ? d[1] + d[2] * T : d[1];   // reactor.py:34-41
         x.fl = d[3];
         if (x.fl != 0.0 && cv.inflow) x.in = cv.inflow[x.gl * cv.ld_in + c * cv.s_in];
+        x.cf[x.gl] = x.cfi;
     }
     wsync();
 }
@@ -441,11 +521,9 @@ __device__ __forceinline__ void grp_setup(const NetView& nv, const CondView& cv,
 // TOF of the group's state (old_system.py:482-488), valid on every lane
 template <int NSP, int G>
 __device__ __forceinline__ double grp_tof(const NetView& nv, const GrpView& g, const Grp<NSP>& x, double y) {
-    wsync();
-    if (x.row) x.c[x.gl] = x.cf * y;
-    wsync();
+    put_c(x, y);
     double t = 0.0;
-    for (int k = x.gl; k < nv.NTOF; k += G) t += rate_net(g, x.kf, x.kr, x.c, nv.tof[k]);
+    for (int k = x.gl; k < nv.NTOF; k += G) t += rec_rate(load_rec(g.rx + nv.tof[k]), x.kf, x.kr, x.c);
     return gsum<G>(t);
 }
 
@@ -469,7 +547,8 @@ __global__ void __launch_bounds__(64) k_solve_grp(NetView nv, GrpView gv, CondVi
     if (q > 0) { pj = (q - 1) >> 1; pfac = (q & 1) ? 1.0 + a.eps : 1.0 - a.eps; }
     Grp<NSP> x;
     double T;
-    grp_setup<NSP, G>(nv, cv, c, kf, kr, ld_k, pj, pfac, lds + (size_t)grp * grp_lds_doubles(nv.NRXN, NSP), x, T);
+    grp_setup<NSP, G>(nv, cv, c, kf, kr, ld_k, pj, pfac,
+                      lds + (size_t)grp * grp_lds_doubles(nv.NRXN, NSP, nv.NDYN), x, T);
     double y = x.row ? cv.y0[x.gl * cv.ld_y0 + c * cv.s_y0] : 0.0;
     int ns = 0;
     int st = grp_integrate<NSP, G>(nv, gv, x, y, a.t0, a.t_end, a.rtol, a.atol, a.max_steps, ns);
@@ -519,14 +598,15 @@ __global__ void __launch_bounds__(64) k_rates_grp(NetView nv, GrpView gv, CondVi
     if (c >= cv.n) return;
     Grp<NSP> x;
     double T;
-    grp_setup<NSP, G>(nv, cv, c, kf, kr, ld_k, -1, 1.0, lds + (size_t)grp * grp_lds_doubles(nv.NRXN, NSP), x, T);
+    grp_setup<NSP, G>(nv, cv, c, kf, kr, ld_k, -1, 1.0, lds + (size_t)grp * grp_lds_doubles(nv.NRXN, NSP, nv.NDYN),
+                      x, T);
     const double y = x.row ? yin[x.gl * ld_y + c] : 0.0;
     if (!jac) {
-        const double f = grp_rhs(gv, x, y);
+        const double f = grp_rhs<NSP, G>(gv, x, y);
         if (x.row) out[x.gl * ld_y + c] = f;
     } else {
         double W[NSP];
-        grp_jac(gv, x, y, 1.0, 0.0, W);
+        grp_jac<NSP, G>(gv, x, y, 1.0, 0.0, W);
         if (x.row) {
 #pragma unroll
             for (int q = 0; q < NSP; ++q)

@@ -30,8 +30,8 @@ struct pck_network {
     int64_t kbuf_cap = 0;
     double* drcbuf = nullptr;       // lane-group DRC: [2R+1][n] TOF + [2R+1][n] status
     int64_t drcbuf_cap = 0;
-    int32_t* d_gi = nullptr;        // sparse plan for the lane-group solver (mk_group.h)
-    double* d_gd = nullptr;
+    GrpRec* d_grx = nullptr;        // lane-group solver (mk_group.h): one record per reaction
+    int grp_ok = 0;                 // every reaction fits a record (<= 6 participants, exponents <= 31)
     GrpView gv;
     int spec = 0;                   // id of the compiled-in plan (networks.h) or 0
     int plan_mode = PCK_PLAN_AUTO;  // pck_network_set_plan_mode
@@ -190,46 +190,52 @@ extern "C" int pck_network_create(const int32_t* ip, int64_t n_ip, const double*
     nv.rxd = Dp + doff[PCK_D_RX]; nv.S = Dp + doff[PCK_D_STOICH]; nv.dyn = Dp + doff[PCK_D_DYN];
     nv.C = Dp + doff[PCK_D_CONS];
     net->nv = nv;
-    // sparse plan for the lane-group solver: participants of each reaction,
-    // CSR of the stoichiometry by species
+    // sparse plan for the lane-group solver (mk_group.h): one record per
+    // reaction (packed participants) and one per nonzero of S, CSR by species
     {
         const int R = nv.NRXN, NS = nv.NDYN;
         const double* S = dp + doff[PCK_D_STOICH];
-        const double* dyn = dp + doff[PCK_D_DYN];
-        std::vector<int32_t> gi, rx_ptr(1, 0), rx_sp, rx_e, row_ptr(1, 0), row_rx;
-        std::vector<double> rx_cf, row_s;
+        std::vector<GrpRec> rx(R > 0 ? R : 1);
+        net->grp_ok = 1;
         for (int j = 0; j < R; ++j) {
+            GrpRec& q = rx[j];
+            memset(&q, 0, sizeof(q));
+            q.r = j;
+            uint32_t w[3] = {0, 0, 0}, sp[3] = {0, 0, 0};
             for (int i = 0; i < NS; ++i) {
                 const int ea = ip[oef + j * NS + i], eb = ip[oer + j * NS + i];
-                if (ea | eb) { rx_sp.push_back(i); rx_e.push_back((ea << 8) | eb); rx_cf.push_back(dyn[4 * i]); }
+                if (ea | eb) {
+                    if (q.np == PCK_GRP_MAX_PART || ea > PCK_GRP_MAX_EXP || eb > PCK_GRP_MAX_EXP) {
+                        net->grp_ok = 0;
+                    } else {
+                        const uint32_t f = (uint32_t)i | ((uint32_t)ea << 6) | ((uint32_t)eb << 11);
+                        w[q.np >> 1] |= f << (16 * (q.np & 1));
+                        ++q.np;
+                    }
+                }
+                if (S[i * R + j] != 0.0) {
+                    if (q.ns == PCK_GRP_MAX_STOICH) {
+                        net->grp_ok = 0;
+                    } else {
+                        sp[q.ns >> 2] |= (uint32_t)i << (8 * (q.ns & 3));
+                        q.s[q.ns] = S[i * R + j];
+                        ++q.ns;
+                    }
+                }
             }
-            rx_ptr.push_back((int32_t)rx_sp.size());
+            q.w0 = w[0]; q.w1 = w[1]; q.w2 = w[2];
+            q.sp0 = sp[0]; q.sp1 = sp[1]; q.sp2 = sp[2];
         }
-        for (int i = 0; i < NS; ++i) {
-            for (int j = 0; j < R; ++j)
-                if (S[i * R + j] != 0.0) { row_rx.push_back(j); row_s.push_back(S[i * R + j]); }
-            row_ptr.push_back((int32_t)row_rx.size());
-        }
-        const size_t o_rxp = 0, o_sp = o_rxp + rx_ptr.size(), o_e = o_sp + rx_sp.size(),
-                     o_rp = o_e + rx_e.size(), o_rr = o_rp + row_ptr.size(), ni = o_rr + row_rx.size();
-        gi.reserve(ni);
-        for (auto* v : {&rx_ptr, &rx_sp, &rx_e, &row_ptr, &row_rx}) gi.insert(gi.end(), v->begin(), v->end());
-        std::vector<double> gd(rx_cf);
-        gd.insert(gd.end(), row_s.begin(), row_s.end());
-        e = hipMalloc(&net->d_gi, sizeof(int32_t) * (gi.size() + 1));
-        if (e == hipSuccess) e = hipMalloc(&net->d_gd, sizeof(double) * (gd.size() + 1));
-        if (e == hipSuccess) e = hipMemcpy(net->d_gi, gi.data(), sizeof(int32_t) * gi.size(), hipMemcpyHostToDevice);
-        if (e == hipSuccess && !gd.empty())
-            e = hipMemcpy(net->d_gd, gd.data(), sizeof(double) * gd.size(), hipMemcpyHostToDevice);
+        GrpRec* drx = nullptr;
+        e = hipMalloc(&drx, sizeof(GrpRec) * rx.size());
+        if (e == hipSuccess) e = hipMemcpy(drx, rx.data(), sizeof(GrpRec) * rx.size(), hipMemcpyHostToDevice);
+        net->d_grx = drx;
         if (e != hipSuccess) {
-            (void)hipFree(net->d_ip); (void)hipFree(net->d_dp); (void)hipFree(net->d_gi); (void)hipFree(net->d_gd);
+            (void)hipFree(net->d_ip); (void)hipFree(net->d_dp); (void)hipFree(drx);
             delete net;
             return fail(PCK_E_HIP, "HIP error: %s (%lld)", hipGetErrorString(e), (long long)e);
         }
-        GrpView& g = net->gv;
-        g.rx_ptr = net->d_gi + o_rxp; g.rx_sp = net->d_gi + o_sp; g.rx_e = net->d_gi + o_e;
-        g.row_ptr = net->d_gi + o_rp; g.row_rx = net->d_gi + o_rr;
-        g.rx_cf = net->d_gd; g.row_s = net->d_gd + rx_cf.size();
+        net->gv.rx = drx;
     }
     // structural digest -> compiled-in plan (same bytes as network.py: structural_digest)
     {
@@ -255,7 +261,7 @@ extern "C" int pck_network_create(const int32_t* ip, int64_t n_ip, const double*
 extern "C" int pck_network_destroy(pck_network* net) {
     if (!net) return PCK_OK;
     (void)hipFree(net->d_ip); (void)hipFree(net->d_dp); (void)hipFree(net->scratch); (void)hipFree(net->kbuf);
-    (void)hipFree(net->d_gi); (void)hipFree(net->d_gd); (void)hipFree(net->drcbuf);
+    (void)hipFree(net->d_grx); (void)hipFree(net->drcbuf);
     delete net;
     return PCK_OK;
 }
@@ -360,10 +366,11 @@ static inline int grp_g(int NS) { return NS <= 16 ? 16 : NS <= 32 ? 32 : 64; }
 
 static int launch_grp_rates(const pck_network* net, const pck_conditions* cond, const double* kf, const double* kr,
                             int64_t ld_k, const double* y, int64_t ld_y, double* out, int jac, hipStream_t s) {
+    if (!net->grp_ok) return fail(PCK_E_SIZE, "lane-group solver: a reaction has more than 6 dynamic participants or stoichiometric species%s", "");
     const int NS = net->nv.NDYN;
     const int per = 64 / grp_g(NS);
     dim3 g((unsigned)((cond->n + per - 1) / per));
-    const size_t shm = sizeof(double) * per * grp_lds_doubles(net->nv.NRXN, grp_nsp(NS));
+    const size_t shm = sizeof(double) * per * grp_lds_doubles(net->nv.NRXN, grp_nsp(NS), NS);
 #define CALL(P, GG) hipLaunchKernelGGL((k_rates_grp<P, GG>), g, dim3(64), shm, s, net->nv, net->gv, cview(cond), kf, kr, ld_k, y, ld_y, out, jac)
     PCK_GRP_SWITCH(NS, CALL)
 #undef CALL
@@ -433,6 +440,8 @@ static int launch_solve(pck_network* net, const pck_conditions* cond, const pck_
     a.max_steps = prm->max_steps; a.newton = prm->newton; a.newton_iters = prm->newton_iters;
     a.want_activity = prm->want_activity;
     if (drc_groups || use_group(net, a.G)) {
+        if (!net->grp_ok)
+            return fail(PCK_E_SIZE, "lane-group solver: a reaction has more than 6 dynamic participants or stoichiometric species%s", "");
         GrpArgs ga;
         ga.M = drc_groups ? drc_groups : 1;
         ga.tofbuf = nullptr;
@@ -448,7 +457,7 @@ static int launch_solve(pck_network* net, const pck_conditions* cond, const pck_
         const int per = 64 / grp_g(NS);
         const int64_t groups = n * ga.M;
         dim3 g((unsigned)((groups + per - 1) / per));
-        const size_t shm = sizeof(double) * per * grp_lds_doubles(R, grp_nsp(NS));
+        const size_t shm = sizeof(double) * per * grp_lds_doubles(R, grp_nsp(NS), NS);
 #define CALL(P, GG) hipLaunchKernelGGL((k_solve_grp<P, GG>), g, dim3(64), shm, s, net->nv, net->gv, cview(cond), kf, kr, n, a, ga)
         PCK_GRP_SWITCH(NS, CALL)
 #undef CALL

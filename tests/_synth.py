@@ -1,0 +1,31 @@
+"""Oracle spec (mk_oracle.load_spec layout) of the synthetic stress network
+at one descriptor vector: the same plain-data network the product builds its
+System from (pycatkin_amd.functions.synthetic), energies evaluated numerically."""
+import numpy as np
+
+from pycatkin_amd.functions.synthetic import synthetic_energies
+
+
+def spec_of(net, desc, T=500.0):
+    E, ts = synthetic_energies(net, desc)
+    states = {}
+    def st(name, typ, **kw):
+        d = dict(name=name, type=typ, mass=None, sigma=None, inertia=None, Gelec=None, Gzpe=None, Gvibr=None,
+                 Gtran=None, Grota=None, Gfree=None, add_to_energy=None, gasdata=None, freq=None, i_freq=None,
+                 scaling=None)
+        d.update(kw); states[name] = d
+    for name, mass, sigma, inertia, _ in net['gases']:
+        st(name, 'gas', mass=mass, sigma=sigma, inertia=np.array([i if i > 1e-12 else 0.0 for i in inertia]), Gelec=0.0)
+    st('s', 'surface', Gelec=0.0)
+    for a in net['adsorbates']:
+        st(a, 'adsorbate', Gelec=E[a])
+    for k, v in ts.items():
+        st(k, 'TS', Gelec=v)
+    reactions = {}
+    for j, (kind, reac, prod) in enumerate(net['reactions']):
+        reactions['R%d' % j] = dict(name='R%d' % j, kind='state', reac_type='adsorption' if kind == 'ads' else 'Arrhenius',
+                                    reversible=True, reactants=list(reac), products=list(prod),
+                                    TS=None if kind == 'ads' else ['TS%d' % j], area=1e-19, scaling=1.0, base=None,
+                                    user={k: None for k in ('dErxn_user', 'dEa_fwd_user', 'dEa_rev_user', 'dGrxn_user', 'dGa_fwd_user', 'dGa_rev_user')})
+    start = {g[0]: g[4] for g in net['gases']}; start['s'] = 1.0
+    return dict(states=states, reactions=reactions, system=dict(times=[0.0, 1e4], T=T, p=1e5, start_state=start, rtol=1e-8, atol=1e-10), reactor=dict(kind='ID'))

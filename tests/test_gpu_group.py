@@ -238,3 +238,71 @@ def test_ch4_transient_vs_oracle(P, inputs, EC, EO, tmax):
     r = s.solve_batch(T=np.array([523.0]), t0=0.0, t_end=tmax, rtol=1e-10, atol=1e-12)
     assert r['status'][0] == 0
     assert close(r['y'][:, 0], yT[perm], rtol=1e-5, floor=1e-11), (r['y'][:, 0], yT[perm])
+
+
+@pytest.fixture(scope='module')
+def synthetic(P):
+    from pycatkin_amd.functions.synthetic import synthetic_system
+    return synthetic_system()
+
+
+def test_synthetic_rates_jacobian_vs_oracle(P, synthetic):
+    """BASELINE configs[4] network (50 dynamic species, 150 reactions, groups
+    of 64 lanes): rates / Jacobian at random states and random descriptors."""
+    from _synth import spec_of
+    sim, net = synthetic
+    plan = sim.plan()
+    dnet = sim.device()
+    assert dnet.NDYN == 50 and dnet.NRXN == 150
+    rng = np.random.default_rng(31)
+    n = 6
+    D = rng.uniform(-0.5, 0.5, (4, n))
+    T = np.linspace(450.0, 650.0, n)
+    y = rng.uniform(0.0, 0.05, (50, n))
+    desc = {'D%d' % k: D[k] for k in range(4)}
+    Tt, p, d, fx, y0, inflow = sim._inputs(dnet, plan, n, T, None, desc, None, None, None)
+    kf, kr = dnet.rate_constants(n, Tt, p, d)
+    f = dnet.species_rates(n, Tt, p, y, kf, kr, d, fx, inflow).cpu().numpy()
+    J = dnet.jacobian(n, Tt, p, y, kf, kr, d, fx, inflow).cpu().numpy()
+    for c in range(n):
+        m = O.ClassicModel(spec_of(net, D[:, c], T[c]), T=T[c])
+        full = m.y0.copy()
+        dyn = [m.idx[nm] for nm in plan.dyn]
+        full[dyn] = y[:, c]
+        fr = m.rhs(full)[dyn]
+        Jr = m.jac(full)[np.ix_(dyn, dyn)]
+        np.testing.assert_allclose(f[:, c], fr, rtol=1e-10, atol=1e-12 * np.abs(fr).max())
+        np.testing.assert_allclose(J[:, :, c], Jr, rtol=1e-10, atol=1e-12 * np.abs(Jr).max())
+
+
+def test_synthetic_steady_vs_oracle(P, synthetic):
+    """512 random-energy conditions in one launch (transient to 1e4 s, then
+    Newton).  About half of the random networks are still drifting along a
+    near-singular slow manifold at t_end (Jacobian condition ~1e17): Newton
+    from there does not converge quadratically -- for the oracle either --
+    and the transient state is kept (status 4).  One regular and one
+    non-regular condition are checked against the oracle (scipy BDF +
+    Newton, ~12 s each on one core)."""
+    from _synth import spec_of
+    sim, net = synthetic
+    plan = sim.plan(('R0',))
+    rng = np.random.default_rng(0)
+    n = 512
+    D = rng.uniform(-0.5, 0.5, (n, 4))
+    r = sim.solve_batch(T=np.full(n, 500.0), desc={'D%d' % k: D[:, k] for k in range(4)}, tof_terms=('R0',),
+                        steady=True, max_steps=20000)
+    st = r['status']
+    assert np.mean(st == 0) > 0.3 and np.mean((st == 0) | (st == 4)) > 0.99, np.unique(st, return_counts=True)
+    dyn = None
+    for c in (np.flatnonzero(st == 0)[0], np.flatnonzero(st == 4)[0]):
+        m = O.ClassicModel(spec_of(net, D[c]), T=500.0)
+        dyn = [m.idx[nm] for nm in plan.dyn]
+        yT, _ = m.solve_odes(rtol=1e-8, atol=1e-10)
+        ys = m.find_steady(yT.copy())
+        assert m.regular == (st[c] == 0)
+        if st[c] == 0:
+            assert close(r['y'][:, c], ys[dyn], rtol=1e-6, floor=1e-14), (c, np.abs(r['y'][:, c] - ys[dyn]).max())
+            tof = m.tof(ys, ['R0'])
+            assert abs(r['tof'][c] - tof) <= 1e-6 * abs(tof) + 1e-12
+        else:   # two integrators' transients on a slow manifold: bounded by their error
+            assert close(r['y'][:, c], yT[dyn], rtol=1e-3, floor=1e-9), (c, np.abs(r['y'][:, c] - yT[dyn]).max())
