@@ -67,6 +67,10 @@ def load():
     if not os.path.isfile(LIB_PATH):
         raise RuntimeError('pycatkin_amd: %s not found -- run `python -c "import __graft_entry__ as g; g.build()"` '
                            '(hipcc --offload-arch=gfx950); there is no CPU fallback' % LIB_PATH)
+    # torch first: its HIP runtime (libamdhip64.so.7, bundled with the wheel) is
+    # then the one our library's libamdhip64.so.7 dependency binds to, so the
+    # process has a single HIP/HSA runtime and device buffers are shared.
+    import torch  # noqa: F401
     lib = C.CDLL(LIB_PATH)
     vp, i64, i32p = C.c_void_p, C.c_int64, C.POINTER(C.c_int32)
     lib.pck_abi_version.restype = C.c_int

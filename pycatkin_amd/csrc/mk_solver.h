@@ -374,7 +374,8 @@ __device__ int integrate(const P& p, const Lane<P::NS>& L, const K& k, double (&
         } else {
             h *= finite ? fmax(0.2, 0.9 * rsqrt(sqrt(en))) : 0.25;
         }
-        if (!(h > 1e-15 * fmax(fabs(t), 1e-300)) && t < t_end) return PCK_ST_STEPFAIL;
+        // scipy's BDF limit: a step below 10 ulp(t) is a failure
+        if (!(h > 2.220446049250313e-15 * fmax(fabs(t), 1e-300)) && t < t_end) return PCK_ST_STEPFAIL;
     }
     return PCK_ST_OK;
 }
