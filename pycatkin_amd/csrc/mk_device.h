@@ -157,29 +157,39 @@ __device__ inline void rate_constants_from_feat(const NetView& nv, double T, con
     }
 }
 
-// In-register LU with partial pivoting (row swaps by predicated selects so
-// every register index stays static).  Returns false on a zero pivot.
+// In-register LU with threshold partial pivoting (row swaps by predicated
+// selects so every register index stays static).  The diagonal is kept
+// unless a row below is more than 1/PIVOT_TAU times larger (the classic
+// threshold rule, growth bounded by (1 + 1/tau)^k); when no lane of the
+// wavefront swaps at column k the select block is skipped (wave vote) and
+// bit k of `swaps` stays clear for the solves.  Returns false on a zero pivot.
+constexpr double PIVOT_TAU = 0.1;
+
 template <int NS>
-__device__ __forceinline__ bool lu(double (&A)[NS][NS], int (&piv)[NS]) {
+__device__ __forceinline__ bool lu(double (&A)[NS][NS], int (&piv)[NS], unsigned& swaps) {
     bool ok = true;
+    swaps = 0u;
 #pragma unroll
     for (int k = 0; k < NS; ++k) {
         int p = k;
-        double best = fabs(A[k][k]);
+        double best = fabs(A[k][k]) / PIVOT_TAU;
 #pragma unroll
         for (int r = k + 1; r < NS; ++r) {
             const double a = fabs(A[r][k]);
             if (a > best) { best = a; p = r; }
         }
         piv[k] = p;
+        if (__any(p != k)) {
+            swaps |= 1u << k;
 #pragma unroll
-        for (int r = k + 1; r < NS; ++r) {
-            const bool sw = (p == r);
+            for (int r = k + 1; r < NS; ++r) {
+                const bool sw = (p == r);
 #pragma unroll
-            for (int q = 0; q < NS; ++q) {
-                const double a = A[k][q], b = A[r][q];
-                A[k][q] = sw ? b : a;
-                A[r][q] = sw ? a : b;
+                for (int q = 0; q < NS; ++q) {
+                    const double a = A[k][q], b = A[r][q];
+                    A[k][q] = sw ? b : a;
+                    A[r][q] = sw ? a : b;
+                }
             }
         }
         const double d = A[k][k];
@@ -198,15 +208,18 @@ __device__ __forceinline__ bool lu(double (&A)[NS][NS], int (&piv)[NS]) {
 }
 
 template <int NS>
-__device__ __forceinline__ void lu_solve(const double (&A)[NS][NS], const int (&piv)[NS], double (&b)[NS]) {
+__device__ __forceinline__ void lu_solve(const double (&A)[NS][NS], const int (&piv)[NS], unsigned swaps,
+                                         double (&b)[NS]) {
 #pragma unroll
     for (int k = 0; k < NS; ++k) {
+        if (swaps & (1u << k)) {
 #pragma unroll
-        for (int r = k + 1; r < NS; ++r) {
-            const bool sw = (piv[k] == r);
-            const double a = b[k], c = b[r];
-            b[k] = sw ? c : a;
-            b[r] = sw ? a : c;
+            for (int r = k + 1; r < NS; ++r) {
+                const bool sw = (piv[k] == r);
+                const double a = b[k], c = b[r];
+                b[k] = sw ? c : a;
+                b[r] = sw ? a : c;
+            }
         }
 #pragma unroll
         for (int r = k + 1; r < NS; ++r) b[r] -= A[r][k] * b[k];

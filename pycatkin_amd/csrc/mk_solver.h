@@ -284,6 +284,7 @@ __device__ int integrate(const P& p, const Lane<P::NS>& L, const K& k, double (&
     double t = t0;
     double W[NS][NS];
     int piv[NS];
+    unsigned sw;
     while (t < t_end) {
         if (nsteps >= max_steps) return PCK_ST_MAXSTEPS;
         ++nsteps;
@@ -297,36 +298,36 @@ __device__ int integrate(const P& p, const Lane<P::NS>& L, const K& k, double (&
             for (int q = 0; q < NS; ++q) W[i][q] = -W[i][q];
             W[i][i] += ig;
         }
-        if (!lu<NS>(W, piv)) { h *= 0.25; continue; }
+        if (!lu<NS>(W, piv, sw)) { h *= 0.25; continue; }
         const double ih = 1.0 / h;
         double k1[NS], k2[NS], k3[NS], k4[NS], k5[NS], u[NS], fu[NS];
 #pragma unroll
         for (int i = 0; i < NS; ++i) k1[i] = F0[i];
-        lu_solve<NS>(W, piv, k1);
+        lu_solve<NS>(W, piv, sw,k1);
 #pragma unroll
         for (int i = 0; i < NS; ++i) u[i] = y[i] + a21 * k1[i];
         rhs(p, L, k, u, fu);
 #pragma unroll
         for (int i = 0; i < NS; ++i) k2[i] = fu[i] + ih * (C21 * k1[i]);
-        lu_solve<NS>(W, piv, k2);
+        lu_solve<NS>(W, piv, sw,k2);
 #pragma unroll
         for (int i = 0; i < NS; ++i) u[i] = y[i] + a31 * k1[i] + a32 * k2[i];
         rhs(p, L, k, u, fu);
 #pragma unroll
         for (int i = 0; i < NS; ++i) k3[i] = fu[i] + ih * (C31 * k1[i] + C32 * k2[i]);
-        lu_solve<NS>(W, piv, k3);
+        lu_solve<NS>(W, piv, sw,k3);
 #pragma unroll
         for (int i = 0; i < NS; ++i) u[i] = y[i] + a41 * k1[i] + a42 * k2[i] + a43 * k3[i];
         rhs(p, L, k, u, fu);
 #pragma unroll
         for (int i = 0; i < NS; ++i) k4[i] = fu[i] + ih * (C41 * k1[i] + C42 * k2[i] + C43 * k3[i]);
-        lu_solve<NS>(W, piv, k4);
+        lu_solve<NS>(W, piv, sw,k4);
 #pragma unroll
         for (int i = 0; i < NS; ++i) u[i] = y[i] + a51 * k1[i] + a52 * k2[i] + a53 * k3[i] + a54 * k4[i];
         rhs(p, L, k, u, fu);
 #pragma unroll
         for (int i = 0; i < NS; ++i) k5[i] = fu[i] + ih * (C51 * k1[i] + C52 * k2[i] + C53 * k3[i] + C54 * k4[i]);
-        lu_solve<NS>(W, piv, k5);
+        lu_solve<NS>(W, piv, sw,k5);
 #pragma unroll
         for (int i = 0; i < NS; ++i) u[i] += k5[i];
         rhs(p, L, k, u, fu);
@@ -334,7 +335,7 @@ __device__ int integrate(const P& p, const Lane<P::NS>& L, const K& k, double (&
 #pragma unroll
         for (int i = 0; i < NS; ++i)
             k5[i] = fu[i] + ih * (C61 * k1[i] + C62 * k2[i] + C63 * k3[i] + C64 * k4[i] + C65 * k5[i]);
-        lu_solve<NS>(W, piv, k5);
+        lu_solve<NS>(W, piv, sw,k5);
         bool finite = true;
         double s = 0.0;
 #pragma unroll
@@ -434,8 +435,9 @@ __device__ int newton(const P& p, const Lane<P::NS>& L, const K& k, double (&y)[
             for (int q = 0; q < NS; ++q) J[i][q] *= sc;
             G[i] = -G[i] * sc;
         }
-        if (!lu<NS>(J, piv)) break;
-        lu_solve<NS>(J, piv, G);
+        unsigned sw;
+        if (!lu<NS>(J, piv, sw)) break;
+        lu_solve<NS>(J, piv, sw, G);
         double alpha = 1.0;
         if (linear >= 2 && lastq < 0.9) {
             alpha = fmin(4.0, 1.0 / (1.0 - lastq));
