@@ -10,7 +10,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, 'libpycatkin_amd.so')
+# PCK_LIB selects an alternative in-tree build (A/B experiments of tools/ab_variants.sh)
+LIB_PATH = os.environ.get('PCK_LIB') or os.path.join(_HERE, 'libpycatkin_amd.so')
 
 # symbols declared in include/pycatkin_amd.h (checked by tests/test_capi.py)
 EXPORTED = ('pck_abi_version', 'pck_last_error', 'pck_network_create', 'pck_network_destroy',

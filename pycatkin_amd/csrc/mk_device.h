@@ -157,6 +157,24 @@ __device__ inline void rate_constants_from_feat(const NetView& nv, double T, con
     }
 }
 
+// Reciprocal from v_rcp_f64 plus two Newton steps (the error of the hardware
+// estimate squares each step: within 1 ulp, not always correctly rounded),
+// 5 VALU ops instead of the ~10 of the IEEE divide sequence.  For positive or
+// negative normal x; used where a last-bit difference only moves a step-size
+// decision or a pivot reciprocal by rounding.
+#ifndef PCK_FASTDIV
+#define PCK_FASTDIV 1
+#endif
+__device__ __forceinline__ double rcp(double x) {
+#if PCK_FASTDIV
+    double r = __builtin_amdgcn_rcp(x);
+    r = fma(fma(-x, r, 1.0), r, r);
+    return fma(fma(-x, r, 1.0), r, r);
+#else
+    return 1.0 / x;
+#endif
+}
+
 // In-register LU with threshold partial pivoting (row swaps by predicated
 // selects so every register index stays static).  The diagonal is kept
 // unless a row below is more than 1/PIVOT_TAU times larger (the classic
@@ -194,7 +212,7 @@ __device__ __forceinline__ bool lu(double (&A)[NS][NS], int (&piv)[NS], unsigned
         }
         const double d = A[k][k];
         ok = ok && (d != 0.0) && (d == d);
-        const double inv = 1.0 / d;
+        const double inv = rcp(d);
 #pragma unroll
         for (int r = k + 1; r < NS; ++r) {
             const double l = A[r][k] * inv;

@@ -15,6 +15,7 @@
 #include "mk_device.h"
 #include "networks.h"
 
+
 namespace pck {
 
 template <int NS_>
@@ -291,7 +292,8 @@ __device__ int integrate(const P& p, const Lane<P::NS>& L, const K& k, double (&
         bool last = false;
         if (t + h >= t_end) { h = t_end - t; last = true; }
         jac(p, L, k, y, W);                               // W = I/(h g) - J
-        const double ig = 1.0 / (h * g);
+        const double ih = rcp(h);
+        const double ig = ih * (1.0 / g);
 #pragma unroll
         for (int i = 0; i < NS; ++i) {
 #pragma unroll
@@ -299,7 +301,6 @@ __device__ int integrate(const P& p, const Lane<P::NS>& L, const K& k, double (&
             W[i][i] += ig;
         }
         if (!lu<NS>(W, piv, sw)) { h *= 0.25; continue; }
-        const double ih = 1.0 / h;
         double k1[NS], k2[NS], k3[NS], k4[NS], k5[NS], u[NS], fu[NS];
 #pragma unroll
         for (int i = 0; i < NS; ++i) k1[i] = F0[i];
@@ -343,7 +344,7 @@ __device__ int integrate(const P& p, const Lane<P::NS>& L, const K& k, double (&
             u[i] += k5[i];
             finite = finite && isfinite(u[i]) && isfinite(k5[i]);
             const double sc = atol + rtol * fmax(fabs(y[i]), fabs(u[i]));
-            const double r = k5[i] / sc;
+            const double r = k5[i] * rcp(sc);
             s += r * r;
         }
         const double en = finite ? sqrt(s / NS) : INFINITY;
@@ -363,7 +364,7 @@ __device__ int integrate(const P& p, const Lane<P::NS>& L, const K& k, double (&
                     sm += p.C(l, i) * y[i];
                 }
                 if (pos && sm > 0.0) {
-                    const double fct = cons0[l] / sm;
+                    const double fct = cons0[l] * rcp(sm);
 #pragma unroll
                     for (int i = 0; i < NS; ++i)
                         if (p.C(l, i) != 0.0) y[i] *= fct;
@@ -563,8 +564,13 @@ struct KFor<PlanCT<Net>> {
     using type = KReg<Net::R>;
 };
 
+// occupancy floor of the solver (waves per SIMD); the VGPR budget follows
+#ifndef PCK_SOLVE_WAVES
+#define PCK_SOLVE_WAVES 1
+#endif
+
 template <class P>
-__global__ void __launch_bounds__(128) k_solve(NetView nv, CondView cv, const double* kf, const double* kr,
+__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(PCK_SOLVE_WAVES))) k_solve(NetView nv, CondView cv, const double* kf, const double* kr,
                                                int64_t ld_k, SolveArgs a) {
     constexpr int NS = P::NS;
     extern __shared__ double lds[];

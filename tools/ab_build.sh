@@ -1,0 +1,14 @@
+#!/bin/bash
+# Build A/B variants of the library (run HERE on the CPU host):
+#   tools/ab_build.sh name1 "-DFLAG=.." name2 "-DFLAG=.." ...
+# -> pycatkin_amd/_ab/lib_<name>.so ; run one with PCK_LIB=<path> python bench.py ...
+set -e
+ROOT=$(cd "$(dirname "$0")/.." && pwd)
+mkdir -p "$ROOT/pycatkin_amd/_ab"
+while [ $# -ge 2 ]; do
+  name=$1; flags=$2; shift 2
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -shared -fPIC $flags -I"$ROOT/include" \
+      -o "$ROOT/pycatkin_amd/_ab/lib_$name.so" "$ROOT/pycatkin_amd/csrc/mk_kernels.hip" &
+done
+wait
+ls -la "$ROOT/pycatkin_amd/_ab"
