@@ -175,6 +175,15 @@ __device__ __forceinline__ double rcp(double x) {
 #endif
 }
 
+// Step-size factor of the error controller, 0.9 en^(-1/4) with en^2 = q the
+// mean squared scaled error, in fp32 (three single-instruction estimates
+// instead of the fp64 sqrt / rsqrt sequences: the factor needs ~3 digits).
+// q = 0 gives +inf and q = inf gives 0; callers clamp to [0.2, 6].
+__device__ __forceinline__ double step_factor(double q) {
+    const float qf = (float)q;
+    return 0.9 * (double)__builtin_amdgcn_rsqf(__builtin_amdgcn_sqrtf(__builtin_amdgcn_sqrtf(qf)));
+}
+
 // In-register LU with threshold partial pivoting (row swaps by predicated
 // selects so every register index stays static).  The diagonal is kept
 // unless a row below is more than 1/PIVOT_TAU times larger (the classic

@@ -256,7 +256,7 @@ __device__ __forceinline__ bool grp_lu(const Grp<NSP>& x, LU<NSP>& F) {
 #pragma unroll
                 for (int j = 1; j < NSP; ++j) x.pb[j] = (j < NSP - k) ? F.W[j] : 0.0;
                 x.perm[k] = p;
-                F.W[0] = 1.0 / F.W[0];
+                F.W[0] = rcp(F.W[0]);
                 fre = false;
                 F.step = k;
             }
@@ -264,7 +264,7 @@ __device__ __forceinline__ bool grp_lu(const Grp<NSP>& x, LU<NSP>& F) {
             const double piv = x.pb[0];
             ok = ok && key >= 0 && piv != 0.0 && isfinite(piv);
             if (ok && fre) {
-                const double l = F.W[0] / piv;
+                const double l = F.W[0] * rcp(piv);
                 F.W[0] = l;
 #pragma unroll
                 for (int j = 1; j < NSP; ++j) F.W[j] -= l * x.pb[j];
@@ -349,10 +349,10 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
         ++nsteps;
         bool last = false;
         if (t + h >= t_end) { h = t_end - t; last = true; }
-        const double ig = 1.0 / (h * g);
+        const double ih = rcp(h);
+        const double ig = ih * (1.0 / g);
         grp_jac<NSP, G>(gv, x, y, -1.0, ig, F.W);        // W = I/(h g) - J
         if (!grp_lu<NSP, G>(x, F)) { h *= 0.25; continue; }
-        const double ih = 1.0 / h;
         const double k1 = grp_solve<NSP, G>(x, F, F0);
         double fu = grp_rhs<NSP, G>(gv, x, y + a21 * k1);
         const double k2 = grp_solve<NSP, G>(x, F, fu + ih * (C21 * k1));
@@ -370,10 +370,11 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
         const bool fin_l = !x.row || (isfinite(u) && isfinite(k6));
         const double fin = gmin<G>(fin_l ? 1.0 : 0.0);
         const double sc = atol + rtol * fmax(fabs(y), fabs(u));
-        const double r = k6 / sc;
+        const double r = k6 * rcp(sc);
         const double s = gsum<G>(x.row ? r * r : 0.0);
-        const double en = (fin > 0.0) ? sqrt(s * invNS) : INFINITY;
-        if (en <= 1.0) {
+        const double q = (fin > 0.0) ? s * invNS : INFINITY;     // en^2
+        const double fac = step_factor(q);
+        if (q <= 1.0) {
             t = last ? t_end : t + h;
             y = x.row ? u : 0.0;
 #pragma unroll
@@ -381,16 +382,15 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
                 if (l < nv.NCONS) {
                     const double sm = gsum<G>(ci[l] * y);
                     if (cpos[l] && sm > 0.0) {
-                        const double fct = cons0[l] / sm;
+                        const double fct = cons0[l] * rcp(sm);
                         if (ci[l] != 0.0) y *= fct;
                     }
                 }
             }
             F0 = grp_rhs<NSP, G>(gv, x, y);
-            const double fac = (en > 0.0) ? 0.9 * rsqrt(sqrt(en)) : 6.0;
             h *= fmin(6.0, fmax(0.2, fac));
         } else {
-            h *= (fin > 0.0) ? fmax(0.2, 0.9 * rsqrt(sqrt(en))) : 0.25;
+            h *= (fin > 0.0) ? fmax(0.2, fac) : 0.25;
         }
         // scipy's BDF limit: a step below 10 ulp(t) is a failure
         if (!(h > 2.220446049250313e-15 * fmax(fabs(t), 1e-300)) && t < t_end) return PCK_ST_STEPFAIL;

@@ -347,8 +347,9 @@ __device__ int integrate(const P& p, const Lane<P::NS>& L, const K& k, double (&
             const double r = k5[i] * rcp(sc);
             s += r * r;
         }
-        const double en = finite ? sqrt(s / NS) : INFINITY;
-        if (en <= 1.0) {
+        const double q = finite ? s * (1.0 / NS) : INFINITY;    // en^2
+        const double fac = step_factor(q);
+        if (q <= 1.0) {
             t = last ? t_end : t + h;
 #pragma unroll
             for (int i = 0; i < NS; ++i) y[i] = u[i];
@@ -371,10 +372,9 @@ __device__ int integrate(const P& p, const Lane<P::NS>& L, const K& k, double (&
                 }
             }
             rhs(p, L, k, y, F0);
-            const double fac = (en > 0.0) ? 0.9 * rsqrt(sqrt(en)) : 6.0;   // 0.9 en^(-1/4)
             h *= fmin(6.0, fmax(0.2, fac));
         } else {
-            h *= finite ? fmax(0.2, 0.9 * rsqrt(sqrt(en))) : 0.25;
+            h *= finite ? fmax(0.2, fac) : 0.25;
         }
         // scipy's BDF limit: a step below 10 ulp(t) is a failure
         if (!(h > 2.220446049250313e-15 * fmax(fabs(t), 1e-300)) && t < t_end) return PCK_ST_STEPFAIL;
