@@ -199,7 +199,7 @@ __device__ __forceinline__ bool lu(double (&A)[NS][NS], int (&piv)[NS], unsigned
 #pragma unroll
     for (int k = 0; k < NS; ++k) {
         int p = k;
-        double best = fabs(A[k][k]) / PIVOT_TAU;
+        double best = fabs(A[k][k]) * (1.0 / PIVOT_TAU);   // a multiply, not an IEEE divide
 #pragma unroll
         for (int r = k + 1; r < NS; ++r) {
             const double a = fabs(A[r][k]);
@@ -234,12 +234,12 @@ __device__ __forceinline__ bool lu(double (&A)[NS][NS], int (&piv)[NS], unsigned
     return ok;
 }
 
-template <int NS>
-__device__ __forceinline__ void lu_solve(const double (&A)[NS][NS], const int (&piv)[NS], unsigned swaps,
-                                         double (&b)[NS]) {
+template <int NS, bool SWAPS>
+__device__ __forceinline__ void lu_solve_impl(const double (&A)[NS][NS], const int (&piv)[NS], unsigned swaps,
+                                              double (&b)[NS]) {
 #pragma unroll
     for (int k = 0; k < NS; ++k) {
-        if (swaps & (1u << k)) {
+        if (SWAPS && (swaps & (1u << k))) {
 #pragma unroll
             for (int r = k + 1; r < NS; ++r) {
                 const bool sw = (piv[k] == r);
@@ -258,6 +258,19 @@ __device__ __forceinline__ void lu_solve(const double (&A)[NS][NS], const int (&
         for (int q = k + 1; q < NS; ++q) v -= A[k][q] * b[q];
         b[k] = v * A[k][k];
     }
+}
+
+// `swaps` is wave-uniform (set under a wave vote in lu): readfirstlane makes
+// that visible to the compiler, so the common no-swap case is one scalar
+// branch to a select-free solve instead of speculated row selects
+template <int NS>
+__device__ __forceinline__ void lu_solve(const double (&A)[NS][NS], const int (&piv)[NS], unsigned swaps,
+                                         double (&b)[NS]) {
+    const unsigned sw = (unsigned)__builtin_amdgcn_readfirstlane((int)swaps);
+    if (sw == 0u)
+        lu_solve_impl<NS, false>(A, piv, 0u, b);
+    else
+        lu_solve_impl<NS, true>(A, piv, sw, b);
 }
 
 }  // namespace pck
