@@ -310,3 +310,21 @@ def test_cooxreactor_sweep_parity(P, inputs, surface):
         assert m.regular
         ref = np.array([ys[m.idx[sp]] for sp in plan.dyn])
         assert close_cov(r['y'][:, k], ref), (T[k], r['y'][:, k], ref)
+
+
+@pytest.mark.parametrize('which, spec', [('Pd111', 2), ('AuPd', 3)])
+def test_compiled_cstr_plan_matches_runtime_plan(P, inputs, which, spec):
+    """k_solve<PlanCT<Cstr*>> (networks.h, examples/COOxReactor) and
+    k_solve<PlanRT<6>> agree on a CSTR temperature sweep (transient + Newton)."""
+    s = P.read_from_input_file(os.path.join(inputs, 'COOxReactor', 'input_%s.json' % which))
+    net = s.device(('CO_ox',))
+    assert net.compiled_plan == spec
+    n = 512
+    kw = dict(T=np.linspace(423.0, 623.0, n), tof_terms=('CO_ox',), steady=True)
+    a = s.solve_batch(**kw)
+    net.set_plan_mode(True)
+    b = s.solve_batch(**kw)
+    net.set_plan_mode(False)
+    assert np.all(a['status'] == 0) and np.all(b['status'] == 0)
+    assert close_cov(a['y'], b['y'], rtol=1e-7, floor=1e-14), np.abs(a['y'] - b['y']).max()
+    np.testing.assert_allclose(a['tof'], b['tof'], rtol=1e-7)

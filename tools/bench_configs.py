@@ -44,12 +44,16 @@ def timed(torch, fn, reps):
     return float(np.mean([a.elapsed_time(b) for a, b in ev])) * 1e-3
 
 
+PLAN_MODE = 0
+
+
 def run(sim, T, desc, tof_terms, steady, drc, reps, torch, t_end=None, rtol=None, atol=None, p=None,
         max_steps=20000, eps=5e-2):
     from pycatkin_amd import _lib as L
     from pycatkin_amd.engine import _ptr
     plan = sim.plan(tuple(tof_terms))
     net = sim.device(tuple(tof_terms))
+    net.set_plan_mode(PLAN_MODE)
     n = len(T)
     Tt, pp, d, fx, y0, inflow = sim._inputs(net, plan, n, T, p, desc, None, None, None)
     cond, keep = net.conditions(n, Tt, pp, d, fx, y0, inflow)
@@ -90,9 +94,12 @@ def main():
     ap.add_argument('--configs', default='cstr,dmtm_drc,synthetic,ch4')
     ap.add_argument('--n', type=int, default=0, help='conditions (0: the config default)')
     ap.add_argument('--reps', type=int, default=3)
+    ap.add_argument('--plan-mode', type=int, default=0, help='0 auto, 1 runtime plan, 2 lane-group solver')
     args = ap.parse_args()
     import torch
     import pycatkin_amd as P
+    global PLAN_MODE
+    PLAN_MODE = args.plan_mode
     lines = []
     for cfg in args.configs.split(','):
         t0 = time.time()
@@ -130,12 +137,14 @@ def main():
         else:
             raise SystemExit('unknown config %s' % cfg)
         r['config'] = cfg
+        r['plan_mode'] = args.plan_mode
         r['wall_s'] = time.time() - t0
         log('%s done in %.1f s' % (cfg, r['wall_s']))
         print(json.dumps(r), flush=True)
         lines.append(r)
     os.makedirs(os.path.join(ROOT, 'gpurun_out'), exist_ok=True)
-    with open(os.path.join(ROOT, 'gpurun_out', 'bench_configs.json'), 'w') as fh:
+    name = 'bench_configs.json' if not args.plan_mode else 'bench_configs_pm%d.json' % args.plan_mode
+    with open(os.path.join(ROOT, 'gpurun_out', name), 'w') as fh:
         json.dump(lines, fh, indent=1)
 
 
