@@ -9,9 +9,19 @@
 // parameter); the per-lane effective rate constants live in LDS so the
 // reaction loop can stay a runtime loop over the plan.
 #pragma once
+#ifdef __HIPCC_RTC__
+// run-time specialisation (mk_jit.h): hipRTC supplies the HIP built-ins and
+// these headers come from the library's embedded copies
+#include <stdint.h>
+#include "pycatkin_amd.h"
+#ifndef INFINITY
+#define INFINITY __builtin_inf()
+#endif
+#else
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "../../include/pycatkin_amd.h"
+#endif
 
 namespace pck {
 

@@ -17,6 +17,7 @@
 #include <vector>
 #include "mk_device.h"
 #include "mk_group.h"
+#include "mk_jit.h"
 
 using namespace pck;
 
@@ -36,6 +37,8 @@ struct pck_network {
     int spec = 0;                   // id of the compiled-in plan (networks.h) or 0
     int plan_mode = PCK_PLAN_AUTO;  // pck_network_set_plan_mode
     unsigned long long digest = 0;
+    std::string jit_src;            // mk_jit.h: constexpr plan source for hipRTC (lane networks without a compiled plan)
+    bool jit_on = false;            // the last lane solve ran the hipRTC-compiled plan
 };
 
 // FNV-1a 64 over the solver-side structure (network.py: structural_digest)
@@ -253,6 +256,9 @@ extern "C" int pck_network_create(const int32_t* ip, int64_t n_ip, const double*
         if (h == T::DIGEST && nv.NDYN == T::NS && nv.NRXN == T::R && nv.NCONS == T::NCONS) net->spec = id;
         PCK_COMPILED_NETWORKS(PCK_MATCH)
 #undef PCK_MATCH
+        if (!net->spec && nv.NDYN >= 1 && nv.NDYN <= PCK_MAX_DYN_LANE)
+            net->jit_src = jit_source(nv.NDYN, nv.NRXN, nv.NCONS, ip + oef, ip + oer, dp + doff[PCK_D_STOICH],
+                                      dp + doff[PCK_D_DYN], dp + doff[PCK_D_CONS], ip + ocp);
     }
     *out = net;
     return PCK_OK;
@@ -271,7 +277,7 @@ extern "C" int pck_network_dims(const pck_network* net, int32_t* dims) {
     const NetView& v = net->nv;
     dims[0] = v.D; dims[1] = v.NTH; dims[2] = v.NREG; dims[3] = v.NRXN; dims[4] = v.NDYN;
     dims[5] = v.NFIX; dims[6] = v.NCONS; dims[7] = v.NTOF; dims[8] = v.nfeat;
-    dims[9] = net->spec;
+    dims[9] = net->spec ? net->spec : net->jit_on ? PCK_SPEC_JIT : 0;
     return PCK_OK;
 }
 
@@ -480,9 +486,23 @@ static int launch_solve(pck_network* net, const pck_conditions* cond, const pck_
         PCK_COMPILED_NETWORKS(PCK_LAUNCH_CT)
 #undef PCK_LAUNCH_CT
     } else {
+        hipFunction_t f = nullptr;
+        if (net->plan_mode == PCK_PLAN_AUTO && !net->jit_src.empty() && jit_enabled())
+            f = jit_kernel(net->digest, net->jit_src);
+        net->jit_on = (f != nullptr);
+        if (f) {
+            NetView nv = net->nv;
+            CondView cv = cview(cond);
+            const double* kfp = kf;
+            const double* krp = kr;
+            int64_t ldk = n;
+            void* args[] = {&nv, &cv, &kfp, &krp, &ldk, &a};
+            HIPCHK(hipModuleLaunchKernel(f, g.x, 1, 1, B, 1, 1, (unsigned)shm, s, args, nullptr));
+        } else {
 #define CALL(N) hipLaunchKernelGGL(k_solve<PlanRT<N>>, g, dim3(B), shm, s, net->nv, cview(cond), kf, kr, n, a)
-        PCK_NS_SWITCH(net->nv.NDYN, CALL)
+            PCK_NS_SWITCH(net->nv.NDYN, CALL)
 #undef CALL
+        }
     }
     HIPCHK(hipGetLastError());
     return PCK_OK;

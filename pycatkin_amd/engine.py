@@ -47,6 +47,13 @@ class DeviceNetwork:
         (self.D, self.NTH, self.NREG, self.NRXN, self.NDYN, self.NFIX, self.NCONS, self.NTOF,
          self.nfeat, self.compiled_plan) = list(dims)
 
+    def plan_id(self):
+        """Solver plan of the last lane solve: a compiled-in id (csrc/networks.h),
+        100 = hipRTC-specialised at run time (csrc/mk_jit.h), 0 = runtime plan."""
+        dims = (C.c_int32 * 10)()
+        L.check(self.lib.pck_network_dims(self.h, dims))
+        return int(dims[9])
+
     def set_plan_mode(self, mode):
         """A/B switch: 0 / False = auto, 1 / True = runtime plan (never the
         compiled-in one), 2 = lane-group solver."""

@@ -328,3 +328,30 @@ def test_compiled_cstr_plan_matches_runtime_plan(P, inputs, which, spec):
     assert np.all(a['status'] == 0) and np.all(b['status'] == 0)
     assert close_cov(a['y'], b['y'], rtol=1e-7, floor=1e-14), np.abs(a['y'] - b['y']).max()
     np.testing.assert_allclose(a['tof'], b['tof'], rtol=1e-7)
+
+
+def test_jit_plan_matches_runtime_plan(P, inputs):
+    """A lane network without a compiled-in plan (the volcano network in a
+    CSTReactor: 6 dynamic species) runs the kernel hipRTC specialises for it at
+    the first solve (csrc/mk_jit.h); it agrees with the runtime plan."""
+    cst = P.CSTReactor(residence_time=4.5, volume=1.8e-7, catalyst_area=3.82e-9)
+    s = volcano_sys(P, inputs, reactor=cst)
+    s.params['inflow_state'] = {'CO': 0.02, 'O2': 0.08}
+    s._plans.clear()
+    net = s.device(('CO_ox',))
+    assert net.compiled_plan == 0
+    rng = np.random.default_rng(11)
+    n = 512
+    kw = dict(T=np.full(n, 600.0), desc={'ECO': rng.uniform(-2.0, 0.0, n), 'EO': rng.uniform(-2.0, 0.0, n)},
+              tof_terms=('CO_ox',), steady=True, t_end=3600.0, rtol=1e-9, atol=1e-13)
+    a = s.solve_batch(**kw)
+    assert net.plan_id() == 100
+    net.set_plan_mode(True)
+    b = s.solve_batch(**kw)
+    assert net.plan_id() == 0
+    net.set_plan_mode(False)
+    both = (a['status'] == 0) & (b['status'] == 0)
+    assert np.mean(both) > 0.9, (np.unique(a['status'], return_counts=True), np.unique(b['status'], return_counts=True))
+    assert np.mean(a['status'] != b['status']) < 0.05
+    assert close_cov(a['y'][:, both], b['y'][:, both], rtol=1e-7, floor=1e-14), np.abs(a['y'] - b['y'])[:, both].max()
+    np.testing.assert_allclose(a['tof'][both], b['tof'][both], rtol=1e-7)

@@ -8,7 +8,7 @@ mkdir -p "$ROOT/pycatkin_amd/_ab"
 while [ $# -ge 2 ]; do
   name=$1; flags=$2; shift 2
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fno-signed-zeros -shared -fPIC $flags -I"$ROOT/include" \
-      -o "$ROOT/pycatkin_amd/_ab/lib_$name.so" "$ROOT/pycatkin_amd/csrc/mk_kernels.hip" &
+      -o "$ROOT/pycatkin_amd/_ab/lib_$name.so" "$ROOT/pycatkin_amd/csrc/mk_kernels.hip" -lhiprtc &
 done
 wait
 ls -la "$ROOT/pycatkin_amd/_ab"
