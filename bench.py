@@ -90,13 +90,18 @@ def log(msg):
 
 
 def profiled_traffic(kernel_name, grid):
-    """HBM bytes per launch of `kernel_name` from the newest committed rocprofv3
-    PMC summary (profiles/r*/*/summary.json, written by tools/pmc_summary.py from
-    a tools/profile.sh run of this bench at the same grid), or (None, None)."""
+    """HBM bytes per launch of `kernel_name` from the committed rocprofv3 PMC
+    summary named in profiles/CURRENT (else the last of profiles/r*/*/summary.json;
+    written by tools/pmc_summary.py from a tools/profile.sh run of this bench at
+    the same grid), or (None, None)."""
     import glob
     key = kernel_name.replace('PlanCT<', 'PlanCT<pck::nets::')
     found = None
-    for f in sorted(glob.glob(os.path.join(ROOT, 'profiles', 'r*', '*', 'summary.json'))):
+    files = sorted(glob.glob(os.path.join(ROOT, 'profiles', 'r*', '*', 'summary.json')))
+    cur = os.path.join(ROOT, 'profiles', 'CURRENT')      # the profile of the current kernel, searched last (wins)
+    if os.path.isfile(cur):
+        files.append(os.path.join(ROOT, open(cur).read().strip(), 'summary.json'))
+    for f in files:
         try:
             s = json.load(open(f))
         except (OSError, ValueError):

@@ -370,7 +370,7 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
         const bool fin_l = !x.row || (isfinite(u) && isfinite(k6));
         const double fin = gmin<G>(fin_l ? 1.0 : 0.0);
         const double sc = atol + rtol * fmax(fabs(y), fabs(u));
-        const double r = k6 * rcp(sc);
+        const double r = k6 * __builtin_amdgcn_rcp(sc);     // error weight: the v_rcp_f64 estimate suffices
         const double s = gsum<G>(x.row ? r * r : 0.0);
         const double q = (fin > 0.0) ? s * invNS : INFINITY;     // en^2
         const double fac = step_factor(q);

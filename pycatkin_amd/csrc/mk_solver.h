@@ -344,7 +344,7 @@ __device__ int integrate(const P& p, const Lane<P::NS>& L, const K& k, double (&
             u[i] += k5[i];
             finite = finite && isfinite(u[i]) && isfinite(k5[i]);
             const double sc = atol + rtol * fmax(fabs(y[i]), fabs(u[i]));
-            const double r = k5[i] * rcp(sc);
+            const double r = k5[i] * __builtin_amdgcn_rcp(sc);   // error weight: the v_rcp_f64 estimate suffices
             s += r * r;
         }
         const double q = finite ? s * (1.0 / NS) : INFINITY;    // en^2
