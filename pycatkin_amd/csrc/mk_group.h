@@ -242,6 +242,42 @@ __device__ __forceinline__ bool grp_lu(const Grp<NSP>& x, LU<NSP>& F) {
     bool fre = x.row;
     bool ok = true;
     F.step = NSP;
+    if constexpr (NSP <= 16) {
+        // unrolled: column k stays in W[k] (static index), no rotation moves,
+        // and only the columns right of k are updated
+#pragma unroll
+        for (int k = 0; k < NSP; ++k) {
+            if (k < x.NS) {
+                const float mag = (float)fabs(F.W[k]);
+                int key = fre ? (int)((__float_as_uint(mag) & ~63u) | (uint32_t)x.gl) : -1;
+                key = gmaxi<G>(key);
+                const int p = key & 63;
+                wsync();
+                if (x.gl == p) {
+                    x.pb[0] = F.W[k];
+#pragma unroll
+                    for (int j = k + 1; j < NSP; ++j) x.pb[j - k] = F.W[j];
+                    x.perm[k] = p;
+                    F.W[k] = rcp(F.W[k]);
+                    fre = false;
+                    F.step = k;
+                }
+                wsync();
+                const double piv = x.pb[0];
+                ok = ok && key >= 0 && piv != 0.0 && isfinite(piv);
+                if (ok && fre) {
+                    const double l = F.W[k] * rcp(piv);
+                    F.W[k] = l;
+#pragma unroll
+                    for (int j = k + 1; j < NSP; ++j) F.W[j] -= l * x.pb[j - k];
+                }
+            }
+        }
+        wsync();
+#pragma unroll
+        for (int q = 0; q < NSP; ++q) F.pk.set(q, q < x.NS ? x.perm[q] : 0);
+        return ok;
+    }
 #pragma unroll 1
     for (int k = 0; k < NSP; ++k) {
         // W[j] holds column (k + j) mod NSP; columns < k sit at j >= NSP - k
