@@ -38,3 +38,15 @@ def test_header_enums_match_python_constants():
     enum = re.search(r'enum \{\s*PCK_I_VERSION = 0,(.*?)PCK_I_HDR', txt, re.S).group(1)
     names = re.findall(r'(PCK_I_[A-Z_]+)', enum)
     assert len(names) + 1 == _lib.I_HDR
+
+
+def test_embedded_rtc_sources_match_headers():
+    """The device headers hipRTC compiles network-specialised solvers from
+    (csrc/rtc_sources.inc, written by build()) are the library's own."""
+    import __graft_entry__ as G
+    inc = os.path.join(os.path.dirname(_lib.LIB_PATH), 'csrc', 'rtc_sources.inc')
+    if not os.path.isfile(inc):
+        pytest.skip('library not built (run __graft_entry__.build())')
+    text = open(inc).read()
+    for name, path in G.RTC_HEADERS:
+        assert open(path).read() in text, name

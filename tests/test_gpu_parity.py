@@ -355,3 +355,23 @@ def test_jit_plan_matches_runtime_plan(P, inputs):
     assert np.mean(a['status'] != b['status']) < 0.05
     assert close_cov(a['y'][:, both], b['y'][:, both], rtol=1e-7, floor=1e-14), np.abs(a['y'] - b['y'])[:, both].max()
     np.testing.assert_allclose(a['tof'][both], b['tof'][both], rtol=1e-7)
+
+
+def test_jit_can_be_disabled(P, inputs, monkeypatch):
+    """PCK_JIT=0: the same network runs the runtime plan (and still agrees)."""
+    cst = P.CSTReactor(residence_time=3.0, volume=1.8e-7, catalyst_area=3.82e-9)
+    s = volcano_sys(P, inputs, reactor=cst)
+    s.params['inflow_state'] = {'CO': 0.03, 'O2': 0.07}
+    s._plans.clear()
+    net = s.device(('CO_ox',))
+    kw = dict(T=np.full(64, 600.0), desc={'ECO': np.linspace(-1.5, -0.5, 64), 'EO': np.linspace(-1.5, -0.5, 64)},
+              tof_terms=('CO_ox',), steady=True, t_end=3600.0, rtol=1e-9, atol=1e-13)
+    monkeypatch.setenv('PCK_JIT', '0')
+    b = s.solve_batch(**kw)
+    assert net.plan_id() == 0
+    monkeypatch.delenv('PCK_JIT')
+    a = s.solve_batch(**kw)
+    assert net.plan_id() == 100
+    ok = (a['status'] == 0) & (b['status'] == 0)
+    assert ok.mean() > 0.9
+    np.testing.assert_allclose(a['tof'][ok], b['tof'][ok], rtol=1e-7)
