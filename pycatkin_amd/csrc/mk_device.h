@@ -213,7 +213,8 @@ __device__ __forceinline__ bool lu(double (&A)[NS][NS], int (&piv)[NS], unsigned
 #pragma unroll
         for (int r = k + 1; r < NS; ++r) {
             const double a = fabs(A[r][k]);
-            if (a > best) { best = a; p = r; }
+            p = (a > best) ? r : p;      // one select + a max instead of selecting a double pair
+            best = fmax(best, a);
         }
         piv[k] = p;
         if (__any(p != k)) {

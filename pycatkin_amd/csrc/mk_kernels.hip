@@ -475,7 +475,7 @@ static int launch_solve(pck_network* net, const pck_conditions* cond, const pck_
         }
         return PCK_OK;
     }
-    const int B = 128;
+    const int B = PCK_SOLVE_BLOCK;
     const int64_t lanes = n * a.G;
     const size_t shm = lds_bytes(R, net->nv.NDYN, B);
     dim3 g((unsigned)((lanes + B - 1) / B));
