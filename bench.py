@@ -122,6 +122,9 @@ def main():
     ap.add_argument('--grid', type=int, default=1024)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-points', type=int, default=160)
+    ap.add_argument('--tile', default='16x4', help='patch shape (rows x cols) of --order tile')
+    ap.add_argument('--order', choices=('tile', 'row'), default='tile',
+                    help="condition order in HBM: 'tile' = one grid patch per wave (default), 'row' = row-major")
     ap.add_argument('--runtime-plan', action='store_true',
                     help='A/B: force the runtime-plan solver instead of the compiled-in network')
     args = ap.parse_args()
@@ -139,7 +142,7 @@ def main():
     import pycatkin_amd as P
     from pycatkin_amd import _lib as L
     from pycatkin_amd.engine import _ptr
-    from pycatkin_amd.functions.volcano import set_volcano_energies
+    from pycatkin_amd.functions.volcano import set_volcano_energies, tile_order
     from pycatkin_amd.parallel import weak_grid_rows
 
     sim = P.read_from_input_file(os.path.join(ROOT, 'tests', 'golden', 'inputs', 'COOxVolcano', 'input.json'))
@@ -153,6 +156,9 @@ def main():
     eco_loc = weak_grid_rows(G, rank, world)        # rank's rows of the (world*G) x G grid
     E1, E2 = np.meshgrid(eco_loc, eo, indexing='ij')
     n = E1.size
+    if args.order == 'tile':                        # one wave = one 16x4 patch of the grid (E_CO x E_O)
+        perm = tile_order(E1.shape, tuple(int(x) for x in args.tile.split('x')))
+        E1, E2 = E1.ravel()[perm], E2.ravel()[perm]
     T = float(sim.params['temperature'])
     Tt, p, d, fx, y0, inflow = sim._inputs(net, plan, n, np.full(n, T), None,
                                            {'ECO': E1.ravel(), 'EO': E2.ravel()}, None, None, None)
