@@ -122,6 +122,10 @@ def main():
     ap.add_argument('--grid', type=int, default=1024)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-points', type=int, default=160)
+    ap.add_argument('--shard', choices=('cyclic', 'contiguous'), default='cyclic',
+                    help='E_CO rows of the (N*G) x G weak-scaling grid per rank: every N-th row (default) or a band')
+    ap.add_argument('--emulate', default=None, metavar='R/N',
+                    help='single-GPU A/B: solve the shard rank R of N would own, without a process group')
     ap.add_argument('--tile', default='16x4', help='patch shape (rows x cols) of --order tile')
     ap.add_argument('--order', choices=('tile', 'row'), default='tile',
                     help="condition order in HBM: 'tile' = one grid patch per wave (default), 'row' = row-major")
@@ -143,7 +147,7 @@ def main():
     from pycatkin_amd import _lib as L
     from pycatkin_amd.engine import _ptr
     from pycatkin_amd.functions.volcano import set_volcano_energies, tile_order
-    from pycatkin_amd.parallel import weak_grid_rows
+    from pycatkin_amd.parallel import assemble_weak_grid, weak_grid_rows
 
     sim = P.read_from_input_file(os.path.join(ROOT, 'tests', 'golden', 'inputs', 'COOxVolcano', 'input.json'))
     set_volcano_energies(sim)
@@ -153,9 +157,12 @@ def main():
     kernel_name = 'k_solve<PlanRT<4>>' if (args.runtime_plan or not net.compiled_plan) else 'k_solve<PlanCT<Volcano>>'
     G = args.grid
     eo = np.linspace(-2.5, 0.5, G)
-    eco_loc = weak_grid_rows(G, rank, world)        # rank's rows of the (world*G) x G grid
+    shard_rank, shard_world = (rank, world) if not args.emulate else map(int, args.emulate.split('/'))
+    cyclic = args.shard == 'cyclic'
+    eco_loc = weak_grid_rows(G, shard_rank, shard_world, cyclic=cyclic)   # rank's rows of the (world*G) x G grid
     E1, E2 = np.meshgrid(eco_loc, eo, indexing='ij')
     n = E1.size
+    perm = None
     if args.order == 'tile':                        # one wave = one 16x4 patch of the grid (E_CO x E_O)
         perm = tile_order(E1.shape, tuple(int(x) for x in args.tile.split('x')))
         E1, E2 = E1.ravel()[perm], E2.ravel()[perm]
@@ -235,6 +242,8 @@ def main():
         # final gather of the activity map (RCCL over xGMI), outside the timed region
         gathered = [torch.empty_like(out['tof']) for _ in range(world)]
         dist.all_gather(gathered, out['tof'])
+        act_map = assemble_weak_grid(gathered, G, G, perm, cyclic)      # (world*G) x G activity map
+        assert act_map.shape == (world * G, G)
         cnt = torch.tensor([n_fail], dtype=torch.int64, device='cuda')
         dist.all_reduce(cnt)
         n_fail = int(cnt)
@@ -259,7 +268,9 @@ def main():
                                     'COOxVolcano network',
             'config': {'workload': 'COOxVolcano %dx%d (E_CO x E_O) grid per GPU, T=600 K, t_end=3600 s, '
                                    'rtol 1e-8 / atol 1e-10, Newton steady-state polish, activity' % (G, G),
-                       'grid_per_gpu': [G, G], 'global_grid': [G * world, G], 'parallelism': 'dp%d' % world},
+                       'grid_per_gpu': [G, G], 'global_grid': [G * world, G], 'parallelism': 'dp%d' % world,
+                       'shard': args.shard + ('' if not args.emulate else ' (emulated rank %s)' % args.emulate),
+                       'order': args.order if args.order == 'row' else 'tile %s' % args.tile},
             'roofline': {'bound': 'valu_fp64', 'achieved': achieved, 'peak': FP64_VECTOR_PEAK_TFLOPS,
                          'unit': 'TFLOP/s', 'frac': achieved / FP64_VECTOR_PEAK_TFLOPS, 'traffic': traffic,
                          'traffic_unit': 'bytes per launch (rocprofv3 PMC FETCH_SIZE x2 + WRITE_SIZE)',

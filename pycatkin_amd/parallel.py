@@ -19,11 +19,22 @@ def shard_bounds(n_total, rank, world):
     return start, start + base + (1 if rank < extra else 0)
 
 
-def weak_grid_rows(rows_per_rank, rank, world, lo=-2.5, hi=0.5):
+def weak_grid_rows(rows_per_rank, rank, world, lo=-2.5, hi=0.5, cyclic=True):
     """The bench's weak-scaling grid axis: world*rows_per_rank points on
-    [lo, hi], of which `rank` owns rows [rank*rows_per_rank, (rank+1)*rows_per_rank)."""
+    [lo, hi].  cyclic (default): `rank` owns rows rank, rank+world, ... -- every
+    rank samples the whole descriptor range, so the per-rank cost matches the
+    one-GPU grid instead of depending on which band of the volcano a rank got;
+    contiguous: rows [rank*rows_per_rank, (rank+1)*rows_per_rank)."""
     axis = np.linspace(lo, hi, rows_per_rank * world)
+    if cyclic:
+        return axis[rank::world]
     return axis[rank * rows_per_rank:(rank + 1) * rows_per_rank]
+
+
+def weak_grid_row_index(rows_per_rank, rank, world, cyclic=True):
+    """Global row numbers of weak_grid_rows(rows_per_rank, rank, world)."""
+    rows = np.arange(rows_per_rank * world)
+    return rows[rank::world] if cyclic else rows[rank * rows_per_rank:(rank + 1) * rows_per_rank]
 
 
 def gather_shards(local, n_total, dist=None, group=None):
@@ -41,3 +52,21 @@ def gather_shards(local, n_total, dist=None, group=None):
     out = [torch.empty_like(buf) for _ in range(world)]
     dist.all_gather(out, buf, group=group)
     return torch.cat([o[:b - a] for o, (a, b) in zip(out, sizes)])
+
+
+def assemble_weak_grid(shards, rows_per_rank, n_cols, perm=None, cyclic=True):
+    """Global (world*rows_per_rank, n_cols) map from every rank's flat result
+    (the list an all_gather returns, rank order).  `perm` is the device order
+    of the local conditions (functions/volcano.py: tile_order), undone first."""
+    import torch
+    world = len(shards)
+    out = torch.empty((rows_per_rank * world, n_cols), dtype=shards[0].dtype, device=shards[0].device)
+    inv = None
+    if perm is not None:
+        inv = np.empty_like(perm)
+        inv[perm] = np.arange(perm.size)
+        inv = torch.from_numpy(inv).to(shards[0].device)
+    for r, s in enumerate(shards):
+        local = (s[inv] if inv is not None else s).reshape(rows_per_rank, n_cols)
+        out[torch.from_numpy(weak_grid_row_index(rows_per_rank, r, world, cyclic)).to(out.device)] = local
+    return out

@@ -8,7 +8,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from pycatkin_amd.parallel import gather_shards, shard_bounds, weak_grid_rows
+from pycatkin_amd.parallel import assemble_weak_grid, gather_shards, shard_bounds, weak_grid_rows
 
 
 def test_shard_bounds_cover_exactly():
@@ -20,10 +20,52 @@ def test_shard_bounds_cover_exactly():
             assert max(y - x for x, y in b) - min(y - x for x, y in b) <= 1
 
 
-def test_weak_grid_rows_partition_the_axis():
+@pytest.mark.parametrize('cyclic', [True, False])
+def test_weak_grid_rows_partition_the_axis(cyclic):
     world, G = 4, 16
-    rows = np.concatenate([weak_grid_rows(G, r, world) for r in range(world)])
-    np.testing.assert_array_equal(rows, np.linspace(-2.5, 0.5, G * world))
+    rows = np.concatenate([weak_grid_rows(G, r, world, cyclic=cyclic) for r in range(world)])
+    np.testing.assert_array_equal(np.sort(rows), np.linspace(-2.5, 0.5, G * world))
+    if cyclic:      # every rank spans the whole descriptor range at the one-GPU spacing
+        for r in range(world):
+            x = weak_grid_rows(G, r, world)
+            assert x[0] <= -2.5 + 3.0 / (G * world) * world and x[-1] >= 0.5 - 3.0 / G
+            np.testing.assert_allclose(np.diff(x), 3.0 / (G * world - 1) * world)
+
+
+def _bench_worker(rank, world, port, q):
+    # bench.py's weak-scaling layout: cyclic E_CO rows per rank, 16x4 patch order
+    # on the device, one all_gather, reassembled into the global grid
+    from pycatkin_amd.functions.volcano import tile_order
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    G, C = 32, 24
+    eco = weak_grid_rows(G, rank, world)
+    eo = np.linspace(-2.5, 0.5, C)
+    E1, E2 = np.meshgrid(eco, eo, indexing='ij')
+    perm = tile_order(E1.shape)
+    val = torch.from_numpy(E1.ravel()[perm] * 10.0 + E2.ravel()[perm])     # stand-in for the activity
+    got = [torch.empty_like(val) for _ in range(world)]
+    dist.all_gather(got, val)
+    if rank == 0:
+        q.put(assemble_weak_grid(got, G, C, perm).numpy().tolist())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_weak_grid_gather_world2_gloo():
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    full = np.array(q.get(timeout=120))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    E1, E2 = np.meshgrid(np.linspace(-2.5, 0.5, 64), np.linspace(-2.5, 0.5, 24), indexing='ij')
+    np.testing.assert_allclose(full, E1 * 10.0 + E2)
 
 
 def _free_port():
