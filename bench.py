@@ -127,7 +127,7 @@ def main():
     ap.add_argument('--emulate', default=None, metavar='R/N',
                     help='single-GPU A/B: solve the shard rank R of N would own, without a process group')
     ap.add_argument('--tile', default='16x4', help='patch shape (rows x cols) of --order tile')
-    ap.add_argument('--order', choices=('tile', 'row'), default='tile',
+    ap.add_argument('--order', choices=('tile', 'row', 'oracle-steps'), default='tile',
                     help="condition order in HBM: 'tile' = one grid patch per wave (default), 'row' = row-major")
     ap.add_argument('--runtime-plan', action='store_true',
                     help='A/B: force the runtime-plan solver instead of the compiled-in network')
@@ -190,6 +190,17 @@ def main():
     def rate_constants_only():
         L.check(net.lib.pck_rate_constants(net.h, C.byref(cond), _ptr(kf), _ptr(kr), n, sp))
 
+    if args.order == 'oracle-steps':
+        # DIAGNOSTIC ONLY (never the bench line's order): sort the conditions by
+        # the step counts of a first solve, heaviest first -- the ceiling of
+        # any a-priori condition ordering
+        step()
+        torch.cuda.synchronize()
+        srt = torch.argsort(out['nsteps'].long() * 4 - out['status'].long(), descending=True).cpu().numpy()
+        E1, E2 = E1.ravel()[srt], E2.ravel()[srt]
+        Tt, p, d, fx, y0, inflow = sim._inputs(net, plan, n, np.full(n, T), None,
+                                               {'ECO': E1.ravel(), 'EO': E2.ravel()}, None, None, None)
+        cond, keep = net.conditions(n, Tt, p, d, fx, y0, inflow)
     log('rank %d: %d conditions, warmup %d' % (rank, n, args.warmup))
     for _ in range(args.warmup):
         step()

@@ -375,3 +375,24 @@ def test_jit_can_be_disabled(P, inputs, monkeypatch):
     ok = (a['status'] == 0) & (b['status'] == 0)
     assert ok.mean() > 0.9
     np.testing.assert_allclose(a['tof'][ok], b['tof'][ok], rtol=1e-7)
+
+
+def test_patch_order_matches_row_order(P, inputs):
+    """functions/volcano.py lays the grid out as 16x4 patches per wavefront and
+    un-permutes the outputs: every condition is solved in its own lane, so the
+    grid must come back point-for-point equal to a row-major solve_batch
+    (ragged 40 x 37 grid: partial patches at both edges)."""
+    from pycatkin_amd.functions.volcano import set_volcano_energies, volcano_activity, volcano_grid
+    s = P.read_from_input_file(os.path.join(inputs, 'COOxVolcano', 'input.json'))
+    be_co, be_o = np.linspace(-2.5, 0.5, 40), np.linspace(-2.5, 0.5, 37)
+    act, r = volcano_activity(s, be_co, be_o, steady=True)
+    set_volcano_energies(s)
+    eco, eo = volcano_grid(be_co, be_o)
+    ref = s.solve_batch(T=np.full(eco.size, float(s.params['temperature'])), desc={'ECO': eco, 'EO': eo},
+                        tof_terms=('CO_ox',), steady=True, activity=True)
+    np.testing.assert_array_equal(r['status'], ref['status'])
+    np.testing.assert_allclose(act.ravel(), ref['tof'], rtol=1e-12, atol=0)
+    np.testing.assert_allclose(r['y'], ref['y'], rtol=1e-10, atol=1e-300)
+    import torch
+    _, rt = volcano_activity(s, be_co, be_o, steady=True, to_numpy=False)      # device outputs, same order
+    assert torch.equal(rt['status'].cpu(), torch.from_numpy(r['status']))
