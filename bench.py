@@ -122,6 +122,7 @@ def main():
     ap.add_argument('--grid', type=int, default=1024)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-points', type=int, default=160)
+    ap.add_argument('--no-newton', action='store_true', help='A/B diagnostic: transient only (not the bench workload)')
     ap.add_argument('--shard', choices=('cyclic', 'contiguous'), default='cyclic',
                     help='E_CO rows of the (N*G) x G weak-scaling grid per rank: every N-th row (default) or a band')
     ap.add_argument('--emulate', default=None, metavar='R/N',
@@ -172,7 +173,7 @@ def main():
     cond, keep = net.conditions(n, Tt, p, d, fx, y0, inflow)       # device-resident inputs
     times = sim.params['times']
     prm = net.params(t0=times[0], t_end=times[-1], rtol=sim.params['rtol'], atol=sim.params['atol'],
-                     max_steps=200000, newton=True, newton_iters=30, activity=True)
+                     max_steps=200000, newton=not args.no_newton, newton_iters=30, activity=True)
     out = dict(y=torch.empty((net.NDYN, n), dtype=torch.float64, device='cuda'),
                tof=torch.empty(n, dtype=torch.float64, device='cuda'),
                status=torch.empty(n, dtype=torch.int32, device='cuda'),

@@ -200,7 +200,10 @@ __device__ __forceinline__ double step_factor(double q) {
 // threshold rule, growth bounded by (1 + 1/tau)^k); when no lane of the
 // wavefront swaps at column k the select block is skipped (wave vote) and
 // bit k of `swaps` stays clear for the solves.  Returns false on a zero pivot.
-constexpr double PIVOT_TAU = 0.1;
+#ifndef PCK_PIVOT_TAU
+#define PCK_PIVOT_TAU 0.1
+#endif
+constexpr double PIVOT_TAU = PCK_PIVOT_TAU;
 
 template <int NS>
 __device__ __forceinline__ bool lu(double (&A)[NS][NS], int (&piv)[NS], unsigned& swaps) {
