@@ -31,7 +31,10 @@
  * All functions return 0 on success and a negative PCK_E_* code on failure;
  * pck_last_error() returns a message for the calling thread.  Device pointers
  * only; `stream` is a hipStream_t (NULL = default stream).  Launches are
- * asynchronous on `stream` unless noted.
+ * asynchronous on `stream` unless noted.  A network handle is read-only after
+ * pck_network_create: every call allocates its own scratch in stream order
+ * on `stream` (hipMallocAsync / hipFreeAsync), so calls on different streams
+ * may share one network.
  */
 #ifndef PYCATKIN_AMD_H
 #define PYCATKIN_AMD_H
@@ -42,7 +45,7 @@
 extern "C" {
 #endif
 
-#define PCK_ABI_VERSION 1
+#define PCK_ABI_VERSION 2
 
 /* error codes */
 #define PCK_OK 0
@@ -207,10 +210,12 @@ int pck_solve(const pck_network* net, const pck_conditions* cond,
 
 /* Degree of rate control for every active reaction (old_system.py:490):
  * xi[j][ld_xi] = (TOF(k_j*(1+eps)) - TOF(k_j*(1-eps))) / (2 eps TOF0).
- * tof0 (optional) receives the unperturbed TOF; status as pck_solve. */
+ * tof0 (optional) receives the unperturbed TOF; status (optional) the worst
+ * status of the 2R+1 solves (PCK_ST_NONFINITE also for a zero / non-finite
+ * TOF0); nsteps (optional) the sum of their integrator steps. */
 int pck_drc(const pck_network* net, const pck_conditions* cond,
             const pck_solve_params* prm, double* xi, int64_t ld_xi,
-            double* tof0, int32_t* status, void* stream);
+            double* tof0, int32_t* status, int32_t* nsteps, void* stream);
 
 #ifdef __cplusplus
 }

@@ -18,7 +18,7 @@ EXPORTED = ('pck_abi_version', 'pck_last_error', 'pck_network_create', 'pck_netw
             'pck_network_dims', 'pck_network_set_plan_mode', 'pck_energies', 'pck_rate_constants', 'pck_species_rates', 'pck_jacobian',
             'pck_solve', 'pck_drc')
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 # header slot indices (must match the enums of include/pycatkin_amd.h)
 I_VERSION, I_NDESC, I_NTH, I_NREG, I_NRXN, I_NDYN, I_NFIX, I_NCONS, I_NTOF = range(9)
@@ -85,7 +85,7 @@ def load():
     lib.pck_species_rates.argtypes = [vp, C.POINTER(Conditions), vp, vp, i64, vp, i64, vp, vp]
     lib.pck_jacobian.argtypes = [vp, C.POINTER(Conditions), vp, vp, i64, vp, i64, vp, vp]
     lib.pck_solve.argtypes = [vp, C.POINTER(Conditions), C.POINTER(SolveParams), C.POINTER(Outputs), vp]
-    lib.pck_drc.argtypes = [vp, C.POINTER(Conditions), C.POINTER(SolveParams), vp, i64, vp, vp, vp]
+    lib.pck_drc.argtypes = [vp, C.POINTER(Conditions), C.POINTER(SolveParams), vp, i64, vp, vp, vp, vp]
     for name in EXPORTED:
         if name not in ('pck_last_error',):
             getattr(lib, name).restype = C.c_int

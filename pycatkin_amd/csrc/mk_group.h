@@ -31,13 +31,23 @@
 
 namespace pck {
 
+#ifdef PCK_TRACE
+// diagnostic builds only (tools/trace_group.py): per-step records of one condition
+#define PCK_TRACE_N 8192
+#define PCK_TRACE_W 8
+__device__ long long pck_trace_cond = -1;
+__device__ int pck_trace_pos = 0;
+__device__ double pck_trace_buf[PCK_TRACE_N * PCK_TRACE_W];
+__device__ double pck_trace_pivmin = 0.0;
+#endif
+
 #define PCK_GRP_MAX_PART 6   // dynamic participants (species with an exponent) per reaction
 #define PCK_GRP_MAX_STOICH 6 // dynamic species with S != 0 per reaction
 #define PCK_GRP_MAX_EXP 31
 
 // One reaction.  Participant k: 16-bit field of w (k < 4: w01 >> 16k, else
 // w2 >> 16(k-4)) = species | ef << 6 | er << 11.  Stoichiometric entry m:
-// species (sp01 >> 8m) & 63 for m < 4, (sp2 >> 8(m-4)) & 63 otherwise, value s[m].
+// species (sp01 >> 8m) & 63 (m < 6), value s[m].
 struct GrpRec {
     int32_t r, np, ns, pad0;
     uint32_t w0, w1, w2, pad1;
@@ -97,6 +107,7 @@ __device__ __forceinline__ double gbcast(double v, int src) {
 template <int NSP>
 struct Grp {
     int gl, NS, R;
+    int64_t cidx;             // condition index (diagnostics)
     bool row;                 // gl < NS
     double* kf; double* kr;   // effective rate constants (fixed species folded, DRC perturbation)
     double* c;                // concentrations c_q = cf_q y_q
@@ -130,9 +141,10 @@ __device__ __forceinline__ int part_field(const RecV& R, int k) {
     const uint32_t f = (k < 4) ? (uint32_t)(R.w01 >> (16 * k)) : (R.w2 >> (16 * (k - 4)));
     return (int)(f & 0xffffu);
 }
+// entries 0..3 in sp0, 4..7 in sp1 (host packing: sp[m >> 2] byte m & 3), so
+// sp01 = sp1:sp0 holds every entry m < 8 at bits 8m
 __device__ __forceinline__ int stoich_species(const RecV& R, int m) {
-    const uint32_t f = (m < 4) ? (uint32_t)(R.sp01 >> (8 * m)) : (R.sp2 >> (8 * (m - 4)));
-    return (int)(f & 63u);
+    return (int)((uint32_t)(R.sp01 >> (8 * m)) & 63u);
 }
 
 __device__ __forceinline__ double rec_rate(const RecV& R, const double* kf, const double* kr, const double* c) {
@@ -265,6 +277,10 @@ __device__ __forceinline__ bool grp_lu(const Grp<NSP>& x, LU<NSP>& F) {
             wsync();
             const double piv = x.pb[0];
             ok = ok && key >= 0 && piv != 0.0 && isfinite(piv);
+#ifdef PCK_TRACE
+            if (k == 0) pck_trace_pivmin = 1e300;
+            if (x.gl == 0) pck_trace_pivmin = fmin(pck_trace_pivmin, fabs(piv));
+#endif
             if (ok && fre) {
                 const double l = F.W[k] * rcp(piv);
                 F.W[k] = l;
@@ -350,7 +366,20 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
         const double ih = rcp(h);
         const double ig = ih * (1.0 / g);
         grp_jac<NSP, G>(gv, x, y, -1.0, ig, F.W);        // W = I/(h g) - J
-        if (!grp_lu<NSP, G>(x, F)) { h *= 0.25; continue; }
+#ifdef PCK_TRACE
+        const bool tr = (x.cidx == pck_trace_cond) && x.gl == 0;
+        auto trace = [&](double q, double luok) {
+            if (!tr) return;
+            const int pos = pck_trace_pos % PCK_TRACE_N;
+            double* rec = pck_trace_buf + (size_t)pos * PCK_TRACE_W;
+            rec[0] = nsteps; rec[1] = t; rec[2] = h; rec[3] = q; rec[4] = luok; rec[5] = pck_trace_pivmin;
+            rec[6] = F0; rec[7] = y;
+            pck_trace_pos = pck_trace_pos + 1;
+        };
+#else
+        auto trace = [&](double, double) {};
+#endif
+        if (!grp_lu<NSP, G>(x, F)) { trace(-1.0, 0.0); h *= 0.25; continue; }
         const double k1 = grp_solve<NSP, G>(x, F, F0);
         double fu = grp_rhs<NSP, G>(gv, x, y + a21 * k1);
         const double k2 = grp_solve<NSP, G>(x, F, fu + ih * (C21 * k1));
@@ -372,6 +401,7 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
         const double s = gsum<G>(x.row ? r * r : 0.0);
         const double q = (fin > 0.0) ? s * invNS : INFINITY;     // en^2
         const double fac = step_factor(q);
+        trace(q, 1.0);
         if (q <= 1.0) {
             t = last ? t_end : t + h;
             y = x.row ? u : 0.0;
@@ -477,6 +507,7 @@ __device__ __forceinline__ void grp_setup(const NetView& nv, const CondView& cv,
                                           Grp<NSP>& x, double& T) {
     const int R = nv.NRXN;
     x.gl = threadIdx.x % G;
+    x.cidx = c;
     x.NS = nv.NDYN;
     x.R = R;
     x.row = x.gl < x.NS;
@@ -530,6 +561,7 @@ struct GrpArgs {
     int M;              // groups per condition: 1, or 2R+1 in DRC mode
     double* tofbuf;     // DRC mode: [M][n] TOF per perturbation
     int32_t* stbuf;     // DRC mode: [M][n] status per perturbation
+    int32_t* nsbuf;     // DRC mode: [M][n] integrator steps per perturbation
 };
 
 template <int NSP, int G>
@@ -559,6 +591,7 @@ __global__ void __launch_bounds__(64) k_solve_grp(NetView nv, GrpView gv, CondVi
         if (x.gl == 0) {
             ga.tofbuf[(int64_t)q * cv.n + c] = tof;
             ga.stbuf[(int64_t)q * cv.n + c] = st;
+            ga.nsbuf[(int64_t)q * cv.n + c] = ns;
         }
         return;
     }
@@ -572,19 +605,24 @@ __global__ void __launch_bounds__(64) k_solve_grp(NetView nv, GrpView gv, CondVi
 
 // DRC combine (old_system.py:490-515): xi_j = (TOF_j+ - TOF_j-) / (2 eps TOF_0)
 __global__ void __launch_bounds__(256) k_drc_combine(int64_t n, int R, double eps, const double* tofbuf,
-                                                     const int32_t* stbuf, double* xi, int64_t ld_xi, double* tof0,
-                                                     int32_t* status) {
+                                                     const int32_t* stbuf, const int32_t* nsbuf, double* xi,
+                                                     int64_t ld_xi, double* tof0, int32_t* status, int32_t* nsteps) {
     const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= n) return;
     const double t0 = tofbuf[c];
     int st = stbuf[c];
+    int ns = nsbuf[c];
     for (int j = 0; j < R; ++j) {
         const double tp = tofbuf[(int64_t)(2 * j + 1) * n + c], tm = tofbuf[(int64_t)(2 * j + 2) * n + c];
         xi[j * ld_xi + c] = (tp - tm) / (2.0 * eps * t0);
         st = max(st, max(stbuf[(int64_t)(2 * j + 1) * n + c], stbuf[(int64_t)(2 * j + 2) * n + c]));
+        ns += nsbuf[(int64_t)(2 * j + 1) * n + c] + nsbuf[(int64_t)(2 * j + 2) * n + c];
     }
+    // a zero or non-finite base TOF makes every xi meaningless
+    if (st == PCK_ST_OK && !(isfinite(t0) && t0 != 0.0)) st = PCK_ST_NONFINITE;
     if (tof0) tof0[c] = t0;
     if (status) status[c] = st;
+    if (nsteps) nsteps[c] = ns;
 }
 
 template <int NSP, int G>

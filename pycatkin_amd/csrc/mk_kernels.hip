@@ -13,6 +13,7 @@
 #include <math.h>
 #include <stdio.h>
 #include <string.h>
+#include <mutex>
 #include <new>
 #include <vector>
 #include "mk_device.h"
@@ -25,12 +26,6 @@ struct pck_network {
     NetView nv;
     int32_t* d_ip = nullptr;
     double* d_dp = nullptr;
-    double* scratch = nullptr;      // feature scratch [nfeat][cap]
-    int64_t scratch_cap = 0;
-    double* kbuf = nullptr;         // kf/kr scratch for pck_solve/pck_drc
-    int64_t kbuf_cap = 0;
-    double* drcbuf = nullptr;       // lane-group DRC: [2R+1][n] TOF + [2R+1][n] status
-    int64_t drcbuf_cap = 0;
     GrpRec* d_grx = nullptr;        // lane-group solver (mk_group.h): one record per reaction
     int grp_ok = 0;                 // every reaction fits a record (<= 6 participants, exponents <= 31)
     GrpView gv;
@@ -74,13 +69,17 @@ static inline CondView cview(const pck_conditions* c) {
 // ----------------------------------------------------------------------------
 // kernel (1)
 // ----------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_rate_constants(NetView nv, CondView cv, double* feat, int64_t fs,
-                                                        double* kf, double* kr, int64_t ld_k) {
+// feat == nullptr: this block's feature columns in LDS (stride blockDim.x),
+// else column c of the HBM scratch (stride fs)
+__global__ void __launch_bounds__(64) k_rate_constants(NetView nv, CondView cv, double* feat, int64_t fs,
+                                                       double* kf, double* kr, int64_t ld_k) {
+    extern __shared__ double lds_feat[];
     const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= cv.n) return;
     const double T = cv.T[c * cv.sT];
     const double p = cv.p[c * cv.sp];
-    double* f = feat + c;
+    double* f = feat ? feat + c : lds_feat + threadIdx.x;
+    if (!feat) fs = blockDim.x;
     thermo_features(nv, T, p, cv.desc + c * cv.s_desc, cv.ld_desc, f, fs);
     for (int j = 0; j < nv.NRXN; ++j) {
         double a, b;
@@ -91,11 +90,13 @@ __global__ void __launch_bounds__(256) k_rate_constants(NetView nv, CondView cv,
 }
 
 // energy-program registers only (free / reaction energies in eV)
-__global__ void __launch_bounds__(256) k_energies(NetView nv, CondView cv, double* feat, int64_t fs, double* out,
-                                                  int64_t ld_out) {
+__global__ void __launch_bounds__(64) k_energies(NetView nv, CondView cv, double* feat, int64_t fs, double* out,
+                                                 int64_t ld_out) {
+    extern __shared__ double lds_feat[];
     const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= cv.n) return;
-    double* f = feat + c;
+    double* f = feat ? feat + c : lds_feat + threadIdx.x;
+    if (!feat) fs = blockDim.x;
     thermo_features(nv, cv.T[c * cv.sT], cv.p[c * cv.sp], cv.desc + c * cv.s_desc, cv.ld_desc, f, fs);
     const int rb = 2 + nv.D + 3 * nv.NTH;
     for (int r = 0; r < nv.NREG; ++r) out[r * ld_out + c] = f[(rb + r) * fs];
@@ -107,6 +108,22 @@ __global__ void __launch_bounds__(256) k_energies(NetView nv, CondView cv, doubl
 // C-ABI
 // ----------------------------------------------------------------------------
 extern "C" int pck_abi_version(void) { return PCK_ABI_VERSION; }
+
+#ifdef PCK_TRACE
+// diagnostic builds only: trace the lane-group integrator of one condition
+extern "C" int pck_trace_set(long long cond) {
+    int zero = 0;
+    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(pck_trace_cond), &cond, sizeof(cond)));
+    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(pck_trace_pos), &zero, sizeof(zero)));
+    return PCK_OK;
+}
+extern "C" int pck_trace_get(double* host, int* pos) {
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpyFromSymbol(pos, HIP_SYMBOL(pck_trace_pos), sizeof(int)));
+    HIPCHK(hipMemcpyFromSymbol(host, HIP_SYMBOL(pck_trace_buf), sizeof(double) * PCK_TRACE_N * PCK_TRACE_W));
+    return PCK_OK;
+}
+#endif
 extern "C" const char* pck_last_error(void) { return g_err; }
 
 extern "C" int pck_network_create(const int32_t* ip, int64_t n_ip, const double* dp, int64_t n_dp,
@@ -266,8 +283,7 @@ extern "C" int pck_network_create(const int32_t* ip, int64_t n_ip, const double*
 
 extern "C" int pck_network_destroy(pck_network* net) {
     if (!net) return PCK_OK;
-    (void)hipFree(net->d_ip); (void)hipFree(net->d_dp); (void)hipFree(net->scratch); (void)hipFree(net->kbuf);
-    (void)hipFree(net->d_grx); (void)hipFree(net->drcbuf);
+    (void)hipFree(net->d_ip); (void)hipFree(net->d_dp); (void)hipFree(net->d_grx);
     delete net;
     return PCK_OK;
 }
@@ -297,25 +313,69 @@ static int check_cond(const pck_network* net, const pck_conditions* c, bool need
     return PCK_OK;
 }
 
-static int ensure(double** buf, int64_t* cap, int64_t need) {
-    if (*cap >= need) return PCK_OK;
-    (void)hipFree(*buf);
-    *buf = nullptr;
-    *cap = 0;
-    HIPCHK(hipMalloc(buf, sizeof(double) * (need > 0 ? need : 1)));
-    *cap = need;
+// Per-call device scratch, stream-ordered: allocated on the caller's stream
+// before the launches that use it and released on the same stream after them
+// (hipFreeAsync in the destructor, on every return path).  Calls on different
+// streams -- or on one stream, back to back -- never share a buffer, so the
+// network handle is read-only after pck_network_create.  The default pool of
+// the device keeps freed blocks (release threshold raised once per device),
+// so repeated calls do not go back to the driver.
+struct StreamScratch {
+    void* p = nullptr;
+    hipStream_t s = nullptr;
+    StreamScratch() = default;
+    StreamScratch(const StreamScratch&) = delete;
+    StreamScratch& operator=(const StreamScratch&) = delete;
+    ~StreamScratch() { if (p) (void)hipFreeAsync(p, s); }
+    template <class T> T* as() const { return static_cast<T*>(p); }
+};
+
+static void pool_keep_blocks() {
+    static std::mutex mu;
+    static unsigned long long done = 0;     // bit per device
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return;
+    std::lock_guard<std::mutex> lk(mu);
+    if (done & (1ULL << dev)) return;
+    done |= 1ULL << dev;
+    hipMemPool_t pool;
+    if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
+        uint64_t thr = ~0ULL;
+        (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
+    }
+}
+
+static int salloc(StreamScratch& b, size_t bytes, hipStream_t s) {
+    pool_keep_blocks();
+    b.s = s;
+    HIPCHK(hipMallocAsync(&b.p, bytes > 0 ? bytes : 8, s));
     return PCK_OK;
 }
 
-static int launch_rate_constants(pck_network* net, const pck_conditions* cond, double* kf, double* kr, int64_t ld_k,
-                                 hipStream_t s) {
+// kernel (1): the feature columns of a block live in LDS when they fit
+// (nfeat x 64 lanes x 8 B <= 64 KiB), else in per-call HBM scratch
+static constexpr int RC_BLOCK = 64;
+static inline bool rc_feat_in_lds(int nfeat) { return (size_t)nfeat * RC_BLOCK * sizeof(double) <= 64 * 1024; }
+
+static int launch_rate_constants(const pck_network* net, const pck_conditions* cond, double* kf, double* kr,
+                                 int64_t ld_k, hipStream_t s) {
     const int64_t n = cond->n;
     if (n == 0) return PCK_OK;
-    int rc = ensure(&net->scratch, &net->scratch_cap, (int64_t)net->nv.nfeat * n);
-    if (rc) return rc;
-    const int B = 256;
-    hipLaunchKernelGGL(k_rate_constants, dim3((unsigned)((n + B - 1) / B)), dim3(B), 0, s, net->nv, cview(cond),
-                       net->scratch, n, kf, kr, ld_k);
+    const int nfeat = net->nv.nfeat;
+    StreamScratch scr;
+    size_t shm = 0;
+    double* feat = nullptr;
+    int64_t fs = 0;
+    if (rc_feat_in_lds(nfeat)) {
+        shm = sizeof(double) * (size_t)nfeat * RC_BLOCK;
+    } else {
+        int rc = salloc(scr, sizeof(double) * (size_t)nfeat * n, s);
+        if (rc) return rc;
+        feat = scr.as<double>();
+        fs = n;
+    }
+    hipLaunchKernelGGL(k_rate_constants, dim3((unsigned)((n + RC_BLOCK - 1) / RC_BLOCK)), dim3(RC_BLOCK), shm, s,
+                       net->nv, cview(cond), feat, fs, kf, kr, ld_k);
     HIPCHK(hipGetLastError());
     return PCK_OK;
 }
@@ -327,12 +387,21 @@ extern "C" int pck_energies(const pck_network* net, const pck_conditions* cond, 
     const int64_t n = cond->n;
     if (n == 0 || net->nv.NREG == 0) return PCK_OK;
     if (!out || ld_out < n) return fail(PCK_E_ARG, "bad energies output%s (ld %lld)", "", ld_out);
-    pck_network* nn = const_cast<pck_network*>(net);
-    rc = ensure(&nn->scratch, &nn->scratch_cap, (int64_t)net->nv.nfeat * n);
-    if (rc) return rc;
-    const int B = 256;
-    hipLaunchKernelGGL(k_energies, dim3((unsigned)((n + B - 1) / B)), dim3(B), 0, (hipStream_t)stream, net->nv,
-                       cview(cond), nn->scratch, n, out, ld_out);
+    const int nfeat = net->nv.nfeat;
+    StreamScratch scr;
+    size_t shm = 0;
+    double* feat = nullptr;
+    int64_t fs = 0;
+    if (rc_feat_in_lds(nfeat)) {
+        shm = sizeof(double) * (size_t)nfeat * RC_BLOCK;
+    } else {
+        rc = salloc(scr, sizeof(double) * (size_t)nfeat * n, (hipStream_t)stream);
+        if (rc) return rc;
+        feat = scr.as<double>();
+        fs = n;
+    }
+    hipLaunchKernelGGL(k_energies, dim3((unsigned)((n + RC_BLOCK - 1) / RC_BLOCK)), dim3(RC_BLOCK), shm,
+                       (hipStream_t)stream, net->nv, cview(cond), feat, fs, out, ld_out);
     HIPCHK(hipGetLastError());
     return PCK_OK;
 }
@@ -342,7 +411,7 @@ extern "C" int pck_rate_constants(const pck_network* net, const pck_conditions* 
     int rc = check_cond(net, cond, false);
     if (rc) return rc;
     if (cond->n > 0 && (!kf || !kr || ld_k < cond->n)) return fail(PCK_E_ARG, "bad kf/kr output%s (ld_k %lld)", "", ld_k);
-    return launch_rate_constants(const_cast<pck_network*>(net), cond, kf, kr, ld_k, (hipStream_t)stream);
+    return launch_rate_constants(net, cond, kf, kr, ld_k, (hipStream_t)stream);
 }
 
 #define PCK_NS_SWITCH(NS, CALL)                                     \
@@ -430,16 +499,17 @@ static int check_params(const pck_solve_params* prm) {
     return PCK_OK;
 }
 
+// kf / kr of the batch go to `kscr` (per-call, stream-ordered): [2][R][n]
 static int launch_solve(pck_network* net, const pck_conditions* cond, const pck_solve_params* prm, SolveArgs a,
-                        hipStream_t s, int drc_groups = 0) {
+                        hipStream_t s, StreamScratch& kscr, int drc_groups = 0) {
     const int64_t n = cond->n;
     if (n == 0) return PCK_OK;
     if (!cond->y0) return fail(PCK_E_ARG, "initial state y0 required%s", "");
     const int R = net->nv.NRXN;
-    int rc = ensure(&net->kbuf, &net->kbuf_cap, 2LL * (R > 0 ? R : 1) * n);
+    int rc = salloc(kscr, sizeof(double) * 2 * (size_t)(R > 0 ? R : 1) * n, s);
     if (rc) return rc;
-    double* kf = net->kbuf;
-    double* kr = net->kbuf + (int64_t)(R > 0 ? R : 1) * n;
+    double* kf = kscr.as<double>();
+    double* kr = kf + (int64_t)(R > 0 ? R : 1) * n;
     rc = launch_rate_constants(net, cond, kf, kr, n, s);
     if (rc) return rc;
     a.t0 = prm->t0; a.t_end = prm->t_end; a.rtol = prm->rtol; a.atol = prm->atol; a.eps = prm->drc_eps;
@@ -452,12 +522,15 @@ static int launch_solve(pck_network* net, const pck_conditions* cond, const pck_
         ga.M = drc_groups ? drc_groups : 1;
         ga.tofbuf = nullptr;
         ga.stbuf = nullptr;
+        ga.nsbuf = nullptr;
+        StreamScratch dscr;
         if (drc_groups) {
             const int64_t m = (int64_t)drc_groups * n;
-            rc = ensure(&net->drcbuf, &net->drcbuf_cap, m + (m + 1) / 2);
+            rc = salloc(dscr, sizeof(double) * m + 2 * sizeof(int32_t) * m, s);
             if (rc) return rc;
-            ga.tofbuf = net->drcbuf;
-            ga.stbuf = (int32_t*)(net->drcbuf + m);
+            ga.tofbuf = dscr.as<double>();
+            ga.stbuf = (int32_t*)(ga.tofbuf + m);
+            ga.nsbuf = ga.stbuf + m;
         }
         const int NS = net->nv.NDYN;
         const int per = 64 / grp_g(NS);
@@ -470,7 +543,7 @@ static int launch_solve(pck_network* net, const pck_conditions* cond, const pck_
         HIPCHK(hipGetLastError());
         if (drc_groups) {
             hipLaunchKernelGGL(k_drc_combine, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, R, a.eps,
-                               ga.tofbuf, ga.stbuf, a.xi, a.ld_xi, a.tof0, a.status);
+                               ga.tofbuf, ga.stbuf, ga.nsbuf, a.xi, a.ld_xi, a.tof0, a.status, a.nsteps);
             HIPCHK(hipGetLastError());
         }
         return PCK_OK;
@@ -520,15 +593,19 @@ extern "C" int pck_solve(const pck_network* net, const pck_conditions* cond, con
     memset(&a, 0, sizeof(a));
     a.y = out->y; a.ld_y = out->ld_y; a.tof = out->tof; a.status = out->status; a.nsteps = out->nsteps;
     a.G = 1;
+    if ((out->kf || out->kr) && cond->n > 0 && (out->ld_k < cond->n || !out->kf || !out->kr))
+        return fail(PCK_E_ARG, "kf/kr dump needs both arrays%s", "");
+    // the network is not modified; const_cast only for the hipRTC bookkeeping flag
     pck_network* nn = const_cast<pck_network*>(net);
-    rc = launch_solve(nn, cond, prm, a, (hipStream_t)stream);
+    StreamScratch kscr;
+    rc = launch_solve(nn, cond, prm, a, (hipStream_t)stream, kscr);
     if (rc) return rc;
     if ((out->kf || out->kr) && cond->n > 0) {
-        if (out->ld_k < cond->n || !out->kf || !out->kr) return fail(PCK_E_ARG, "kf/kr dump needs both arrays%s", "");
         const int R = net->nv.NRXN;
-        HIPCHK(hipMemcpy2DAsync(out->kf, sizeof(double) * out->ld_k, nn->kbuf, sizeof(double) * cond->n,
+        const double* kb = kscr.as<double>();
+        HIPCHK(hipMemcpy2DAsync(out->kf, sizeof(double) * out->ld_k, kb, sizeof(double) * cond->n,
                                 sizeof(double) * cond->n, R, hipMemcpyDeviceToDevice, (hipStream_t)stream));
-        HIPCHK(hipMemcpy2DAsync(out->kr, sizeof(double) * out->ld_k, nn->kbuf + (int64_t)R * cond->n,
+        HIPCHK(hipMemcpy2DAsync(out->kr, sizeof(double) * out->ld_k, kb + (int64_t)(R > 0 ? R : 1) * cond->n,
                                 sizeof(double) * cond->n, sizeof(double) * cond->n, R, hipMemcpyDeviceToDevice,
                                 (hipStream_t)stream));
     }
@@ -536,7 +613,7 @@ extern "C" int pck_solve(const pck_network* net, const pck_conditions* cond, con
 }
 
 extern "C" int pck_drc(const pck_network* net, const pck_conditions* cond, const pck_solve_params* prm, double* xi,
-                       int64_t ld_xi, double* tof0, int32_t* status, void* stream) {
+                       int64_t ld_xi, double* tof0, int32_t* status, int32_t* nsteps, void* stream) {
     int rc = check_cond(net, cond, true);
     if (rc) return rc;
     rc = check_params(prm);
@@ -548,10 +625,10 @@ extern "C" int pck_drc(const pck_network* net, const pck_conditions* cond, const
     while (G < 2 * R + 1) G <<= 1;
     SolveArgs a;
     memset(&a, 0, sizeof(a));
-    a.xi = xi; a.ld_xi = ld_xi; a.tof0 = tof0; a.status = status; a.G = G;
+    a.xi = xi; a.ld_xi = ld_xi; a.tof0 = tof0; a.status = status; a.nsteps = nsteps; a.G = G;
     pck_network* nn = const_cast<pck_network*>(net);
+    StreamScratch kscr;
     // lane-group networks: one group per (condition, perturbation), combined after
-    if (use_group(net, G)) return launch_solve(nn, cond, prm, a, (hipStream_t)stream, 2 * R + 1);
-    if (status && cond->n > 0) HIPCHK(hipMemsetAsync(status, 0, sizeof(int32_t) * cond->n, (hipStream_t)stream));
-    return launch_solve(nn, cond, prm, a, (hipStream_t)stream);
+    if (use_group(net, G)) return launch_solve(nn, cond, prm, a, (hipStream_t)stream, kscr, 2 * R + 1);
+    return launch_solve(nn, cond, prm, a, (hipStream_t)stream, kscr);
 }

@@ -597,6 +597,7 @@ __global__ void __launch_bounds__(PCK_SOLVE_BLOCK) __attribute__((amdgpu_waves_p
     }
     double tof = 0.0;
     int st = PCK_ST_OK;
+    int ns = 0;
     double T = 0.0;
     if (active) {
         int pj = -1;
@@ -609,15 +610,14 @@ __global__ void __launch_bounds__(PCK_SOLVE_BLOCK) __attribute__((amdgpu_waves_p
         double y[NS];
 #pragma unroll
         for (int i = 0; i < NS; ++i) y[i] = cv.y0[i * cv.ld_y0 + c * cv.s_y0];
-        int ns = 0;
         st = integrate(p, L, k, y, a.t0, a.t_end, a.rtol, a.atol, a.max_steps, ns);
         if (st == PCK_ST_OK && a.newton) st = newton(p, L, k, y, a.newton_iters);
         tof = lane_tof(p, nv, k, y);
-        if (!drc) {
-            bool fin = isfinite(tof);
+        bool fin = isfinite(tof);
 #pragma unroll
-            for (int i = 0; i < NS; ++i) fin = fin && isfinite(y[i]);
-            if (!fin && st == PCK_ST_OK) st = PCK_ST_NONFINITE;
+        for (int i = 0; i < NS; ++i) fin = fin && isfinite(y[i]);
+        if (!fin && st == PCK_ST_OK) st = PCK_ST_NONFINITE;
+        if (!drc) {
             if (a.y) {
 #pragma unroll
                 for (int i = 0; i < NS; ++i) a.y[i * a.ld_y + c] = y[i];
@@ -632,22 +632,29 @@ __global__ void __launch_bounds__(PCK_SOLVE_BLOCK) __attribute__((amdgpu_waves_p
     }
     if (drc) {
         // wavefront-shuffle combine: every lane of a condition's group lives in
-        // the same wavefront (G divides 64)
+        // the same wavefront (G divides 64); the group's status is the worst
+        // member's and its step count the sum (butterfly over the G lanes, so
+        // every lane holds the same values -- no atomics, no pre-zeroed output)
         const int lane = threadIdx.x & 63;
         const int base = lane - q;
         const double t0 = __shfl(tof, base, 64);
         const double tm = __shfl(tof, lane + 1 < 64 ? lane + 1 : lane, 64);
-        const int s0 = __shfl(st, base, 64);
-        const int sm = __shfl(st, lane + 1 < 64 ? lane + 1 : lane, 64);
+        int gst = active ? st : 0;
+        int gns = active ? ns : 0;
+        for (int m = 1; m < G; m <<= 1) {
+            gst = max(gst, __shfl_xor(gst, m, 64));
+            gns += __shfl_xor(gns, m, 64);
+        }
         if (active && (q & 1)) {
             const int j = (q - 1) >> 1;
             a.xi[j * a.ld_xi + c] = (tof - tm) / (2.0 * a.eps * t0);   // old_system.py:508
-            // status of the group = worst member
-            if (a.status && (st | sm)) atomicMax(&a.status[c], st > sm ? st : sm);
         }
         if (active && q == 0) {
+            // a zero or non-finite base TOF makes every xi meaningless
+            if (gst == PCK_ST_OK && !(isfinite(t0) && t0 != 0.0)) gst = PCK_ST_NONFINITE;
             if (a.tof0) a.tof0[c] = tof;
-            if (a.status && s0) atomicMax(&a.status[c], s0);
+            if (a.status) a.status[c] = gst;
+            if (a.nsteps) a.nsteps[c] = gns;
         }
     }
 }

@@ -192,10 +192,11 @@ class DeviceNetwork:
         prm = self.params(**kw)
         xi = torch.zeros((max(self.NRXN, 1), n), dtype=torch.float64, device='cuda')
         tof0 = torch.empty(n, dtype=torch.float64, device='cuda')
-        st = torch.zeros(n, dtype=torch.int32, device='cuda')
-        L.check(self.lib.pck_drc(self.h, C.byref(c), C.byref(prm), _ptr(xi), n, _ptr(tof0), _ptr(st),
+        st = torch.empty(n, dtype=torch.int32, device='cuda')
+        ns = torch.empty(n, dtype=torch.int32, device='cuda')
+        L.check(self.lib.pck_drc(self.h, C.byref(c), C.byref(prm), _ptr(xi), n, _ptr(tof0), _ptr(st), _ptr(ns),
                                  _stream(torch)))
-        return dict(xi=xi[:self.NRXN], tof0=tof0, status=st)
+        return dict(xi=xi[:self.NRXN], tof0=tof0, status=st, nsteps=ns)
 
 
 _form_cache = {}
