@@ -23,6 +23,8 @@
  *                          System.get_dydt / _fun_ss          pycatkin/classes/system.py:396,528
  *   pck_jacobian        <- System.species_jacobian + Reactor.jacobian old_system.py:293, reactor.py:103,161
  *                          System.get_jacobian / _jac_ss      system.py:493,547
+ *   pck_reaction_rates  <- System._calc_rates                 system.py:345
+ *                          System.reaction_terms              old_system.py:202
  *   pck_solve           <- System.solve_odes (+ find_steady)  old_system.py:315 (385)
  *                          SteadyStateSolver.solve_ode        pycatkin/classes/solver.py:374
  *                          System.run_and_return_tof / activity old_system.py:470,517
@@ -197,6 +199,15 @@ int pck_rate_constants(const pck_network* net, const pck_conditions* cond,
 int pck_species_rates(const pck_network* net, const pck_conditions* cond,
                       const double* kf, const double* kr, int64_t ld_k,
                       const double* y, int64_t ld_y, double* dydt, void* stream);
+
+/* Forward and reverse rate of every active reaction at states y ([NS][ld_y]),
+ * fixed-species concentrations folded in: rf, rr [NRXN][ld_r].
+ * Replaces System._calc_rates (pycatkin/classes/system.py:345) and
+ * System.reaction_terms (pycatkin/classes/old_system.py:202). */
+int pck_reaction_rates(const pck_network* net, const pck_conditions* cond,
+                       const double* kf, const double* kr, int64_t ld_k,
+                       const double* y, int64_t ld_y, double* rf, double* rr, int64_t ld_r,
+                       void* stream);
 
 /* Jacobian d(dydt)/dy: jac[(i*NS + k)][ld_y] (row-major per condition). */
 int pck_jacobian(const pck_network* net, const pck_conditions* cond,

@@ -15,8 +15,8 @@ LIB_PATH = os.environ.get('PCK_LIB') or os.path.join(_HERE, 'libpycatkin_amd.so'
 
 # symbols declared in include/pycatkin_amd.h (checked by tests/test_capi.py)
 EXPORTED = ('pck_abi_version', 'pck_last_error', 'pck_network_create', 'pck_network_destroy',
-            'pck_network_dims', 'pck_network_set_plan_mode', 'pck_energies', 'pck_rate_constants', 'pck_species_rates', 'pck_jacobian',
-            'pck_solve', 'pck_drc')
+            'pck_network_dims', 'pck_network_set_plan_mode', 'pck_energies', 'pck_rate_constants', 'pck_species_rates',
+            'pck_reaction_rates', 'pck_jacobian', 'pck_solve', 'pck_drc')
 
 ABI_VERSION = 2
 
@@ -84,6 +84,7 @@ def load():
     lib.pck_rate_constants.argtypes = [vp, C.POINTER(Conditions), vp, vp, i64, vp]
     lib.pck_species_rates.argtypes = [vp, C.POINTER(Conditions), vp, vp, i64, vp, i64, vp, vp]
     lib.pck_jacobian.argtypes = [vp, C.POINTER(Conditions), vp, vp, i64, vp, i64, vp, vp]
+    lib.pck_reaction_rates.argtypes = [vp, C.POINTER(Conditions), vp, vp, i64, vp, i64, vp, vp, i64, vp]
     lib.pck_solve.argtypes = [vp, C.POINTER(Conditions), C.POINTER(SolveParams), C.POINTER(Outputs), vp]
     lib.pck_drc.argtypes = [vp, C.POINTER(Conditions), C.POINTER(SolveParams), vp, i64, vp, vp, vp, vp]
     for name in EXPORTED:

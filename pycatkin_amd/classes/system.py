@@ -134,7 +134,159 @@ class System:
             self.reactor.set_indices([1 if i in ads else 0 for i in range(n)], [1 if i in gas else 0 for i in range(n)])
             self.dynamic_indices = self.reactor.get_dynamic_indices(self.adsorbate_indices, self.gas_indices)
 
-    build = names_to_indices
+    def build(self):
+        """Index bookkeeping: old_system.py:99-152 (classic) or system.py:167-187
+        (patched: coverage_map, gas_indices, index_map, rate_map,
+        initial_system, reaction_matrix)."""
+        if self.formulation == 'patched':
+            return self._build_patched()
+        return self.names_to_indices()
+
+    # -- patched-formulation API (pycatkin/classes/system.py) --------------------
+    def _build_patched(self):
+        """system.py:191-394: index_map (gas first, then each surface followed by
+        its adsorbates), coverage_map {surface: set of indices}, gas_indices,
+        rate_map, initial_system (normalised, capped at min_tol) and the +-1
+        reaction_matrix (species x non-ghost reactions, products win)."""
+        order = self.index_map_ordered()
+        self.index_map = {s: i for i, s in enumerate(order)}
+        self.gas_indices = {i for i, s in enumerate(order) if self.states[s].state_type == 'gas'}
+        self.coverage_map = {sf: {self.index_map[x] for x in grp} for sf, grp in self._coverage_names.items()}
+        self.rate_map = {}
+        for name, rx in self.reactions.items():
+            if str(rx.reac_type).upper() == 'GHOST':
+                continue
+            self.rate_map[name] = {'reac': [self.index_map[x.name] for x in rx.reactants],
+                                   'prod': [self.index_map[x.name] for x in rx.products],
+                                   'site_density': 1.0 / rx.area if rx.area else 0.0, 'scaling': rx.scaling}
+        self.initial_system = self.initial_vector()
+        M = np.zeros((len(order), len(self.rate_map)))
+        for j, rm in enumerate(self.rate_map.values()):
+            M[rm['reac'], j] = -1.0
+            M[rm['prod'], j] = 1.0
+        self.reaction_matrix = M
+        return self
+
+    def _patched_eval(self):
+        if self.formulation != 'patched':
+            raise RuntimeError('the System._fun_ss / get_dydt family belongs to the patched formulation '
+                               '(System(formulation="patched"), pycatkin/classes/system.py)')
+        if getattr(self, 'initial_system', None) is None:
+            self._build_patched()
+        plan = self.plan()
+        net = self.device()
+        ngas = len(self.gas_indices)
+        return plan, net, ngas
+
+    def _device_state(self, plan, y_full):
+        """(surface part in plan.dyn order, gas concentrations x p in plan.fix order)."""
+        y_full = np.asarray(y_full, float).ravel()
+        idx = self.index_map
+        yd = np.array([y_full[idx[s]] for s in plan.dyn])
+        fx = np.array([y_full[idx[s]] for s in plan.fix]) * float(self.p)
+        return yd, fx
+
+    def _rates_batch(self, Y):
+        """forward / backward rates [n_reactions, m] (rate_map order) at full
+        compositions Y [n_species, m] (gas fractions x p), one device launch."""
+        plan, net, ngas = self._patched_eval()
+        Y = np.asarray(Y, float)
+        m = Y.shape[1]
+        idx = self.index_map
+        yd = Y[[idx[s] for s in plan.dyn]]
+        fx = Y[[idx[s] for s in plan.fix]] * float(self.p)
+        T, p = float(self.T), float(self.p)
+        kf, kr = net.rate_constants(m, np.full(m, T), p)
+        rf, rr = net.reaction_rates(m, np.full(m, T), p, yd, kf, kr, None, fx)
+        rf, rr = rf.cpu().numpy(), rr.cpu().numpy()
+        names = list(self.rate_map)
+        order = [plan.reactions.index(name) for name in names]
+        return rf[order], rr[order]
+
+    def _calc_rates(self, y):
+        """system.py:345-376: (n_reactions, 2) forward / backward rates at the
+        full composition y (gas fractions x p), on the device."""
+        rf, rr = self._rates_batch(np.asarray(y, float).reshape(-1, 1))
+        return np.stack([rf[:, 0], rr[:, 0]], axis=1)
+
+    def get_dydt(self, y):
+        """system.py:396-416: reaction_matrix @ (r_fwd - r_rev) for every tracked species."""
+        rates = self._calc_rates(y)
+        return self.reaction_matrix @ (rates[:, 0] - rates[:, 1])
+
+    def get_forward_only(self, y):
+        """system.py:418-433 (the reference multiplies by the backward column)."""
+        return self.reaction_matrix @ self._calc_rates(y)[:, 1]
+
+    def _jac(self, y):
+        """system.py:437-491: d r_j / d y_k (n_reactions x n_species).  Every
+        species enters a side of a reaction with exponent 1 (a repeated species
+        with its count), so d(k prod c)/d y_k = k prod(others) (x p for a gas):
+        the rate of that side with y_k set to 1 -- one device launch evaluates
+        the rates at all n_species such compositions."""
+        self._patched_eval()
+        y = np.asarray(y, float).ravel()
+        n = len(y)
+        Y = np.repeat(y[:, None], n, axis=1)
+        Y[np.arange(n), np.arange(n)] = 1.0
+        rf, rr = self._rates_batch(Y)
+        out = np.zeros((len(self.rate_map), n))
+        for j, (name, rm) in enumerate(self.rate_map.items()):
+            for lst, other, sgn, r in ((rm['reac'], rm['prod'], 1.0, rf), (rm['prod'], rm['reac'], -1.0, rr)):
+                for i in set(lst):
+                    if i in other:
+                        raise RuntimeError('Species %d appreas on both sides of reaction %s' % (i, name))
+                    cnt = lst.count(i)
+                    # side rate at y_i = 1 is k prod(others) y_i^0 -> times cnt y_i^(cnt-1)
+                    out[j, i] = sgn * r[j, i] * (cnt * y[i] ** (cnt - 1) if cnt > 1 else 1.0)
+        return out
+
+    def get_jacobian(self, y):
+        """system.py:493-508: reaction_matrix @ _jac(y)."""
+        return self.reaction_matrix @ self._jac(y)
+
+    def _ss_pre(self, y_surf):
+        """system.py:512-526"""
+        self._patched_eval()
+        y_gas = self.initial_system[sorted(self.gas_indices)]
+        return np.concatenate([y_gas, np.asarray(y_surf, float)])
+
+    def _fun_ss(self, y_surf):
+        """system.py:528-545: surface rates at the invariant gas composition (device pck_species_rates)."""
+        return self._fun_ss_batch(np.asarray(y_surf, float)[:, None])[:, 0]
+
+    def _jac_ss(self, y_surf):
+        """system.py:547-564: surface block of the Jacobian (device pck_jacobian)."""
+        return self._jac_ss_batch(np.asarray(y_surf, float)[:, None])[:, :, 0]
+
+    def _fun_ss_batch(self, Y):
+        """_fun_ss for a batch of surface states Y [n_surface, n] in one launch."""
+        plan, net, ngas = self._patched_eval()
+        n = Y.shape[1]
+        T, p, d, fx, y0, inflow = self._inputs(net, plan, n, float(self.T), None, None, None, None, None)
+        kf, kr = net.rate_constants(n, T, p, d)
+        return net.species_rates(n, T, p, self._to_plan(plan, Y), kf, kr, d, fx, inflow).cpu().numpy()[self._from_plan(plan)]
+
+    def _jac_ss_batch(self, Y):
+        plan, net, ngas = self._patched_eval()
+        n = Y.shape[1]
+        T, p, d, fx, y0, inflow = self._inputs(net, plan, n, float(self.T), None, None, None, None, None)
+        kf, kr = net.rate_constants(n, T, p, d)
+        J = net.jacobian(n, T, p, self._to_plan(plan, Y), kf, kr, d, fx, inflow).cpu().numpy()
+        inv = self._from_plan(plan)
+        return J[np.ix_(inv, inv)]
+
+    def _surface_order(self):
+        return [s for s in sorted(self.index_map, key=self.index_map.get) if self.index_map[s] not in self.gas_indices]
+
+    def _to_plan(self, plan, Y):
+        """surface states in index_map order -> plan.dyn order"""
+        order = self._surface_order()
+        return np.asarray(Y, float)[[order.index(s) for s in plan.dyn]]
+
+    def _from_plan(self, plan):
+        """permutation taking plan.dyn order back to index_map order"""
+        return [plan.dyn.index(s) for s in self._surface_order()]
 
     # -- patched-formulation bookkeeping (system.py:191-328) -------------------
     def index_map_ordered(self):
@@ -142,10 +294,10 @@ class System:
         gas = sorted(n for n, s in self.states.items() if s.state_type == 'gas')
         surf = sorted(n for n, s in self.states.items() if s.state_type == 'surface')
         order = list(gas)
-        self.coverage_map = {}
+        self._coverage_names = {}
         for sf in surf:
             grp = [sf] + [a for a in ads if a[0] == sf]
-            self.coverage_map[sf] = grp
+            self._coverage_names[sf] = grp
             order += grp
         return order
 
@@ -160,7 +312,7 @@ class System:
         gi = [pos[s] for s in order if self.states[s].state_type == 'gas']
         if gi:
             y[gi] /= np.sum(y[gi])
-        for grp in self.coverage_map.values():
+        for grp in self._coverage_names.values():
             ii = [pos[s] for s in grp]
             y[ii] /= np.sum(y[ii])
         return np.where(y < self.min_tol, self.min_tol, y)

@@ -6,25 +6,30 @@
 //
 //   * lane i of a group owns species i: y_i, every Rosenbrock stage entry and
 //     row i of the iteration matrix (NSP doubles in VGPRs, static indices);
-//   * rates and the Jacobian are evaluated lane-per-reaction (reactions gl,
-//     gl+G, ...: balanced whatever the species degrees) from the group's
-//     concentration vector in LDS, and scattered into the species rates /
-//     the [NS][NS] Jacobian block with LDS fp64 atomics
-//     (pycatkin/classes/old_system.py:202-313, system.py:345-508);
+//     NSP = NS exactly when the kernel is specialised for the network's size
+//     at run time (csrc/mk_jit.h), else the next compiled-in size;
+//   * rates: lane-per-reaction (reactions gl, gl+G, ...: balanced whatever the
+//     species degrees) into the group's net-rate buffer in LDS, then every
+//     row lane gathers its own row of S . net from the species CSR of the
+//     stoichiometric matrix (pycatkin/classes/old_system.py:202-248,
+//     system.py:345-416);
+//   * Jacobian: lane-per-reaction derivatives d net_r / d y_q into LDS, then
+//     every row lane accumulates its own row of S . D into a column block of
+//     the group's Jacobian buffer, in P column passes (old_system.py:250-313,
+//     system.py:437-508).  A buffer row is only ever touched by its owner
+//     lane, whose LDS adds execute in program order: the sums are bitwise
+//     reproducible (no cross-lane atomics);
 //   * dense LU with partial pivoting across the group: the pivot is an integer
 //     max-reduction of |a| (float bits, lane id in the low 6 bits), the pivot
-//     row is broadcast through LDS, every free row eliminates its own entries.
-//     The column loop is unrolled, so column k is the static register W[k]
-//     and only the columns right of k are updated (a rolled variant that
-//     rotated each row by one column per step measured 1.37x slower on the
-//     50-species network and 13 % slower on DMTM);
+//     row is broadcast through LDS, every free row eliminates its own entries
+//     (unrolled: column k is the static register W[k]);
 //   * triangular solves: one broadcast per column (v_readlane on a full
 //     wavefront, __shfl on 16/32-lane groups);
 //   * norms / step-size decisions are butterfly all-reductions, bitwise equal
 //     on every lane, so control flow is group-uniform.
 //
-// LDS per group (doubles): kf[R] kr[R] | c[NSP] | cf[NSP] | f[NSP] | pivot row[NSP] |
-// perm[NSP] (int) | J[NS][NS]
+// LDS per group (doubles, each block even-sized): kf[R] kr[R] | c[NSP] |
+// d[max(ND, R)] (net rates / derivatives) | J[NS][QB] | pb[NSP]
 #pragma once
 #include "mk_device.h"
 #include "mk_solver.h"
@@ -38,27 +43,24 @@ namespace pck {
 __device__ long long pck_trace_cond = -1;
 __device__ int pck_trace_pos = 0;
 __device__ double pck_trace_buf[PCK_TRACE_N * PCK_TRACE_W];
-__device__ double pck_trace_pivmin = 0.0;
 #endif
 
 #define PCK_GRP_MAX_PART 6   // dynamic participants (species with an exponent) per reaction
-#define PCK_GRP_MAX_STOICH 6 // dynamic species with S != 0 per reaction
 #define PCK_GRP_MAX_EXP 31
 
-// One reaction.  Participant k: 16-bit field of w (k < 4: w01 >> 16k, else
-// w2 >> 16(k-4)) = species | ef << 6 | er << 11.  Stoichiometric entry m:
-// species (sp01 >> 8m) & 63 (m < 6), value s[m].
-struct GrpRec {
-    int32_t r, np, ns, pad0;
-    uint32_t w0, w1, w2, pad1;
-    uint32_t sp0, sp1, sp2, pad2;
-    uint32_t pad3[4];
-    double s[PCK_GRP_MAX_STOICH];
-};
-static_assert(sizeof(GrpRec) == 112, "GrpRec layout");
-
+// Device tables of the lane-group plan (built by pck_network_create).
+//   rx[R]: {w0, w1, w2, dptr | np << 16}; participant k < np is the 16-bit
+//          field k of w0:w1:w2 = species | ef << 6 | er << 11, and its
+//          derivative lives at d[dptr + k]
+//   row[NS+1], ent[nnz(S)]: CSR of the stoichiometric matrix by species;
+//          entry {a = r | np << 9 | dptr << 12 | q5 << 26,
+//                 b = q0 | q1 << 6 | q2 << 12 | q3 << 18 | q4 << 24, s (lo, hi)}
+//          with q0..q5 the participants of reaction r (as in rx[r])
 struct GrpView {
-    const GrpRec* rx;        // NRXN records
+    const uint4* rx;
+    const int32_t* row;
+    const uint4* ent;
+    int ND;                  // total participants = size of the derivative buffer
 };
 
 __device__ __forceinline__ void wsync() {
@@ -103,54 +105,25 @@ __device__ __forceinline__ double gbcast(double v, int src) {
     }
 }
 
-// Per-group context: LDS blocks and this lane's species row.
-template <int NSP>
-struct Grp {
-    int gl, NS, R;
-    int64_t cidx;             // condition index (diagnostics)
-    bool row;                 // gl < NS
-    double* kf; double* kr;   // effective rate constants (fixed species folded, DRC perturbation)
-    double* c;                // concentrations c_q = cf_q y_q
-    double* cf;               // concentration factors
-    double* f;                // species-rate accumulator
-    double* pb;               // pivot-row broadcast
-    int* perm;                // perm[k] = lane whose row was the pivot of column k
-    double* J;                // Jacobian block, column-major: J[q*NS + i]
-    double cfi, rs, fl, in;   // this row's concentration factor, row scale, flow, inflow
-};
-
-// register copy of a record's index words (no indexed arrays -> no scratch)
-struct RecV {
-    int r, np, ns;
-    uint64_t w01;
-    uint32_t w2;
-    uint64_t sp01;
-    uint32_t sp2;
-};
-__device__ __forceinline__ RecV load_rec(const GrpRec* p) {
-    const uint4 a = *reinterpret_cast<const uint4*>(p);
-    const uint4 b = *(reinterpret_cast<const uint4*>(p) + 1);
-    const uint4 c = *(reinterpret_cast<const uint4*>(p) + 2);
-    RecV v;
-    v.r = (int)a.x; v.np = (int)a.y; v.ns = (int)a.z;
-    v.w01 = ((uint64_t)b.y << 32) | b.x; v.w2 = b.z;
-    v.sp01 = ((uint64_t)c.y << 32) | c.x; v.sp2 = c.z;
-    return v;
+__device__ __forceinline__ int rx_np(const uint4& r) { return (int)((r.w >> 16) & 7u); }
+__device__ __forceinline__ int rx_dptr(const uint4& r) { return (int)(r.w & 0xffffu); }
+__device__ __forceinline__ int rx_field(const uint4& r, int k) {
+    const uint32_t w = (k < 2) ? r.x : (k < 4) ? r.y : r.z;
+    return (int)((w >> (16 * (k & 1))) & 0xffffu);
 }
-__device__ __forceinline__ int part_field(const RecV& R, int k) {
-    const uint32_t f = (k < 4) ? (uint32_t)(R.w01 >> (16 * k)) : (R.w2 >> (16 * (k - 4)));
-    return (int)(f & 0xffffu);
-}
-// entries 0..3 in sp0, 4..7 in sp1 (host packing: sp[m >> 2] byte m & 3), so
-// sp01 = sp1:sp0 holds every entry m < 8 at bits 8m
-__device__ __forceinline__ int stoich_species(const RecV& R, int m) {
-    return (int)((uint32_t)(R.sp01 >> (8 * m)) & 63u);
+__device__ __forceinline__ double ent_s(const uint4& e) { return __hiloint2double((int)e.w, (int)e.z); }
+__device__ __forceinline__ int ent_r(const uint4& e) { return (int)(e.x & 511u); }
+__device__ __forceinline__ int ent_np(const uint4& e) { return (int)((e.x >> 9) & 7u); }
+__device__ __forceinline__ int ent_dptr(const uint4& e) { return (int)((e.x >> 12) & 0x3fffu); }
+__device__ __forceinline__ int ent_species(const uint4& e, int k) {
+    return (k < 5) ? (int)((e.y >> (6 * k)) & 63u) : (int)(e.x >> 26);
 }
 
-__device__ __forceinline__ double rec_rate(const RecV& R, const double* kf, const double* kr, const double* c) {
-    double a = kf[R.r], b = kr[R.r];
-    for (int k = 0; k < R.np; ++k) {
-        const int f = part_field(R, k);
+// net rate of a reaction (record rec) from the group's concentrations
+__device__ __forceinline__ double rec_rate(const uint4& rec, double a, double b, const double* c) {
+    const int np = rx_np(rec);
+    for (int k = 0; k < np; ++k) {
+        const int f = rx_field(rec, k);
         const double x = c[f & 63];
         const int ef = (f >> 6) & 31, er = f >> 11;
         if (ef) a *= ipow(x, ef);
@@ -160,16 +133,16 @@ __device__ __forceinline__ double rec_rate(const RecV& R, const double* kf, cons
 }
 
 // d(net_r)/d(c_q) for participant k0 of the record's reaction
-__device__ __forceinline__ double rec_drate(const RecV& R, const double* kf, const double* kr, const double* c,
-                                            int k0) {
-    const int f0 = part_field(R, k0);
+__device__ __forceinline__ double rec_drate(const uint4& rec, double kf, double kr, const double* c, int k0) {
+    const int np = rx_np(rec);
+    const int f0 = rx_field(rec, k0);
     const int ef0 = (f0 >> 6) & 31, er0 = f0 >> 11;
     const double x0 = c[f0 & 63];
-    double a = ef0 ? kf[R.r] * (double)ef0 * ipow(x0, ef0 - 1) : 0.0;
-    double b = er0 ? kr[R.r] * (double)er0 * ipow(x0, er0 - 1) : 0.0;
-    for (int k = 0; k < R.np; ++k) {
+    double a = ef0 ? kf * (double)ef0 * ipow(x0, ef0 - 1) : 0.0;
+    double b = er0 ? kr * (double)er0 * ipow(x0, er0 - 1) : 0.0;
+    for (int k = 0; k < np; ++k) {
         if (k == k0) continue;
-        const int f = part_field(R, k);
+        const int f = rx_field(rec, k);
         const double x = c[f & 63];
         const int ef = (f >> 6) & 31, er = f >> 11;
         if (ef) a *= ipow(x, ef);
@@ -178,10 +151,31 @@ __device__ __forceinline__ double rec_drate(const RecV& R, const double* kf, con
     return a - b;
 }
 
+__host__ __device__ constexpr int grp_even(int n) { return (n + 1) & ~1; }
+__host__ __device__ inline size_t grp_lds_doubles(int R, int NSP, int NS, int ND, int QB) {
+    const int r1 = R > 0 ? R : 1;
+    return (size_t)2 * grp_even(r1) + grp_even(NSP) + grp_even(ND > r1 ? ND : r1) + grp_even(NS * QB) + grp_even(NSP);
+}
+
+// Per-group context: LDS blocks and this lane's species row.
+template <int NSP>
+struct Grp {
+    int gl, NS, R, QB;
+    int64_t cidx;             // condition index (diagnostics)
+    bool row;                 // gl < NS
+    double* kf; double* kr;   // effective rate constants (fixed species folded, DRC perturbation)
+    double* c;                // concentrations c_q = cf_q y_q
+    double* d;                // net rates [R] / derivatives [ND]
+    double* J;                // Jacobian column block: J[i*QB + j]
+    double* pb;               // pivot-row broadcast
+    int rb, re;               // this row's CSR range
+    double cfi, rs, fl, in;   // this row's concentration factor, row scale, flow, inflow
+};
+
 template <int NSP>
 __device__ __forceinline__ void put_c(const Grp<NSP>& x, double y) {
-    wsync();                                   // previous readers of c / f are done
-    if (x.row) { x.c[x.gl] = x.cfi * y; x.f[x.gl] = 0.0; }
+    wsync();                                   // previous readers of c / d are done
+    if (x.row) x.c[x.gl] = x.cfi * y;
     wsync();
 }
 
@@ -189,43 +183,77 @@ __device__ __forceinline__ void put_c(const Grp<NSP>& x, double y) {
 template <int NSP, int G>
 __device__ __forceinline__ double grp_rhs(const GrpView& g, const Grp<NSP>& x, double y) {
     put_c(x, y);
-    for (int j = x.gl; j < x.R; j += G) {
-        const GrpRec* p = g.rx + j;
-        const RecV R = load_rec(p);
-        const double net = rec_rate(R, x.kf, x.kr, x.c);
-        for (int m = 0; m < R.ns; ++m) atomicAdd(x.f + stoich_species(R, m), p->s[m] * net);
-    }
+    for (int r = x.gl; r < x.R; r += G) x.d[r] = rec_rate(g.rx[r], x.kf[r], x.kr[r], x.c);
     wsync();
-    return x.row ? x.f[x.gl] * x.rs + x.fl * (x.in - y) : 0.0;
+    double f = 0.0;
+    if (x.row) {
+        // two partial sums and a 4-deep unroll keep several entry loads in flight
+        double f2 = 0.0;
+        int e = x.rb;
+#pragma unroll 2
+        for (; e + 1 < x.re; e += 2) {
+            const uint4 q = g.ent[e], q2 = g.ent[e + 1];
+            f = fma(ent_s(q), x.d[ent_r(q)], f);
+            f2 = fma(ent_s(q2), x.d[ent_r(q2)], f2);
+        }
+        if (e < x.re) {
+            const uint4 q = g.ent[e];
+            f = fma(ent_s(q), x.d[ent_r(q)], f);
+        }
+        f = (f + f2) * x.rs + x.fl * (x.in - y);
+    }
+    return f;
 }
 
 // W[q] = sgn * dF_i/dy_q + (q == i ? shift : 0), with dF/dy including the flow
-// diagonal (-fl_i).  The block is read back and cleared.
-template <int NSP, int G>
-__device__ __forceinline__ void grp_jac(const GrpView& g, const Grp<NSP>& x, double y, double sgn, double shift,
-                                        double (&W)[NSP]) {
+// diagonal (-fl_i); 0 on lanes without a row
+template <int NSP, int G, int P>
+__device__ __forceinline__ void grp_jac(const NetView& nv, const GrpView& g, const Grp<NSP>& x, double y, double sgn,
+                                        double shift, double (&W)[NSP]) {
+    constexpr int QB = (NSP + P - 1) / P;
     put_c(x, y);
-    const int NS = x.NS;
-    for (int j = x.gl; j < x.R; j += G) {
-        const GrpRec* p = g.rx + j;
-        const RecV R = load_rec(p);
-        for (int k = 0; k < R.np; ++k) {
-            const int q = part_field(R, k) & 63;
-            const double d = rec_drate(R, x.kf, x.kr, x.c, k) * x.cf[q];
-            for (int m = 0; m < R.ns; ++m) atomicAdd(x.J + q * NS + stoich_species(R, m), p->s[m] * d);
+    for (int r = x.gl; r < x.R; r += G) {
+        const uint4 rec = g.rx[r];
+        const int np = rx_np(rec), dp = rx_dptr(rec);
+        const double a = x.kf[r], b = x.kr[r];
+        for (int k = 0; k < np; ++k) {
+            const int q = rx_field(rec, k) & 63;
+            x.d[dp + k] = rec_drate(rec, a, b, x.c, k) * nv.dyn[4 * q];     // x cf_q
         }
     }
     wsync();
     const double sc = sgn * x.rs;
     const double dg = shift - sgn * x.fl;
 #pragma unroll
-    for (int q = 0; q < NSP; ++q) {
-        double v = 0.0;
-        if (q < NS && x.row) {
-            v = x.J[q * NS + x.gl];
-            x.J[q * NS + x.gl] = 0.0;
+    for (int pass = 0; pass < P; ++pass) {
+        const int q0 = pass * QB;
+        if (x.row) {
+            double* jr = x.J + x.gl * QB - q0;
+#pragma unroll 4
+            for (int e = x.rb; e < x.re; ++e) {
+                const uint4 q = g.ent[e];
+                const double s = ent_s(q);
+                const int np = ent_np(q), dp = ent_dptr(q);
+                for (int k = 0; k < np; ++k) {
+                    const int sp = ent_species(q, k);
+                    // only the owner lane adds to its row: program order = summation order
+                    if (P == 1 || (sp >= q0 && sp < q0 + QB)) atomicAdd(jr + sp, s * x.d[dp + k]);
+                }
+            }
         }
-        W[q] = sc * v + (q == x.gl ? dg : 0.0);
+        wsync();
+#pragma unroll
+        for (int j = 0; j < QB; ++j) {
+            const int q = q0 + j;
+            if (q < NSP) {
+                double v = 0.0;
+                if (x.row && q < x.NS) {
+                    v = x.J[x.gl * QB + j];
+                    x.J[x.gl * QB + j] = 0.0;
+                }
+                W[q] = x.row ? sc * v + (q == x.gl ? dg : 0.0) : 0.0;
+            }
+        }
     }
 }
 
@@ -255,8 +283,6 @@ __device__ __forceinline__ bool grp_lu(const Grp<NSP>& x, LU<NSP>& F) {
     bool fre = x.row;
     bool ok = true;
     F.step = NSP;
-    // unrolled: column k stays in W[k] (static index), no rotation moves,
-    // and only the columns right of k are updated
 #pragma unroll
     for (int k = 0; k < NSP; ++k) {
         if (k < x.NS) {
@@ -264,34 +290,49 @@ __device__ __forceinline__ bool grp_lu(const Grp<NSP>& x, LU<NSP>& F) {
             int key = fre ? (int)((__float_as_uint(mag) & ~63u) | (uint32_t)x.gl) : -1;
             key = gmaxi<G>(key);
             const int p = key & 63;
-            wsync();
-            if (x.gl == p) {
-                x.pb[0] = F.W[k];
+            if constexpr (G == 64) {
+                // full wavefront: the pivot row is read straight out of the
+                // pivot lane's registers (v_readlane into SGPRs, used as the
+                // scalar operand of the FMAs) -- no LDS round trip, no copy
+                const int ps = __builtin_amdgcn_readfirstlane(p);
+                const double piv = gbcast<64>(F.W[k], ps);
+                ok = ok && key >= 0 && piv != 0.0 && isfinite(piv);
+                const bool elim = ok && fre && x.gl != ps;
+                if (x.gl == ps) {
+                    F.W[k] = rcp(F.W[k]);
+                    fre = false;
+                    F.step = k;
+                }
+                if (elim) {
+                    const double l = F.W[k] * rcp(piv);
+                    F.W[k] = l;
 #pragma unroll
-                for (int j = k + 1; j < NSP; ++j) x.pb[j - k] = F.W[j];
-                x.perm[k] = p;
-                F.W[k] = rcp(F.W[k]);
-                fre = false;
-                F.step = k;
-            }
-            wsync();
-            const double piv = x.pb[0];
-            ok = ok && key >= 0 && piv != 0.0 && isfinite(piv);
-#ifdef PCK_TRACE
-            if (k == 0) pck_trace_pivmin = 1e300;
-            if (x.gl == 0) pck_trace_pivmin = fmin(pck_trace_pivmin, fabs(piv));
-#endif
-            if (ok && fre) {
-                const double l = F.W[k] * rcp(piv);
-                F.W[k] = l;
+                    for (int j = k + 1; j < NSP; ++j) F.W[j] -= l * gbcast<64>(F.W[j], ps);
+                }
+            } else {
+                wsync();                           // readers of the previous pivot row are done
+                if (x.gl == p) {
 #pragma unroll
-                for (int j = k + 1; j < NSP; ++j) F.W[j] -= l * x.pb[j - k];
+                    for (int j = k; j < NSP; ++j) x.pb[j - k] = F.W[j];
+                }
+                wsync();
+                const double piv = x.pb[0];
+                ok = ok && key >= 0 && piv != 0.0 && isfinite(piv);
+                if (x.gl == p) {
+                    F.W[k] = rcp(F.W[k]);
+                    fre = false;
+                    F.step = k;
+                }
+                if (ok && fre) {
+                    const double l = F.W[k] * rcp(piv);
+                    F.W[k] = l;
+#pragma unroll
+                    for (int j = k + 1; j < NSP; ++j) F.W[j] -= l * x.pb[j - k];
+                }
             }
+            F.pk.set(k, p);
         }
     }
-    wsync();
-#pragma unroll
-    for (int q = 0; q < NSP; ++q) F.pk.set(q, q < x.NS ? x.perm[q] : 0);
     return ok;
 }
 
@@ -319,12 +360,13 @@ __device__ __forceinline__ double grp_solve(const Grp<NSP>& x, const LU<NSP>& F,
 }
 
 // ---------------------------------------------------------------------------
-// RODAS4 on the group (same scheme, controller and projection as mk_solver.h)
+// RODAS4 on the group (same scheme, controller, projection and positivity
+// rule as mk_solver.h: integrate)
 // ---------------------------------------------------------------------------
-template <int NSP, int G>
+template <int NSP, int G, int P>
 __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& gv, const Grp<NSP>& x, double& y,
                                              double t0, double t_end, double rtol, double atol, int max_steps,
-                                             int& nsteps) {
+                                             int& nsteps, bool crows) {
     using namespace rodas4;
     const int NS = x.NS;
     const double invNS = 1.0 / NS;
@@ -358,6 +400,12 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
     }
     double t = t0;
     LU<NSP> F;
+    int blowups = 0;
+    int stall = 0;
+    int cpv = -1;                                              // conservation law whose pivot row is this lane's
+    for (int l = 0; l < nv.NCONS; ++l)
+        if (crows && x.row && nv.cpiv[l] == x.gl) cpv = l;
+    const double keep = (cpv >= 0) ? 0.0 : 1.0;                // its stage right-hand sides are 0
     while (t < t_end) {
         if (nsteps >= max_steps) return PCK_ST_MAXSTEPS;
         ++nsteps;
@@ -365,34 +413,48 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
         if (t + h >= t_end) { h = t_end - t; last = true; }
         const double ih = rcp(h);
         const double ig = ih * (1.0 / g);
-        grp_jac<NSP, G>(gv, x, y, -1.0, ig, F.W);        // W = I/(h g) - J
+        grp_jac<NSP, G, P>(nv, gv, x, y, -1.0, ig, F.W);       // W = I/(h g) - J
+        if (cpv >= 0) {                                        // conservation rows (mk_solver.h: cons_rows)
+            double m = 0.0;
+#pragma unroll
+            for (int q = 0; q < NSP; ++q) m = fmax(m, fabs(F.W[q]));
+#pragma unroll
+            for (int q = 0; q < NSP; ++q) F.W[q] = (q < NS) ? nv.C[cpv * NS + q] * m : 0.0;
+        }
 #ifdef PCK_TRACE
         const bool tr = (x.cidx == pck_trace_cond) && x.gl == 0;
+        const double ymin = gmin<G>(x.row ? y : INFINITY);
         auto trace = [&](double q, double luok) {
             if (!tr) return;
             const int pos = pck_trace_pos % PCK_TRACE_N;
             double* rec = pck_trace_buf + (size_t)pos * PCK_TRACE_W;
-            rec[0] = nsteps; rec[1] = t; rec[2] = h; rec[3] = q; rec[4] = luok; rec[5] = pck_trace_pivmin;
+            rec[0] = nsteps; rec[1] = t; rec[2] = h; rec[3] = q; rec[4] = luok; rec[5] = ymin;
             rec[6] = F0; rec[7] = y;
             pck_trace_pos = pck_trace_pos + 1;
         };
 #else
         auto trace = [&](double, double) {};
 #endif
-        if (!grp_lu<NSP, G>(x, F)) { trace(-1.0, 0.0); h *= 0.25; continue; }
-        const double k1 = grp_solve<NSP, G>(x, F, F0);
+        if (!grp_lu<NSP, G>(x, F)) {
+            trace(-1.0, 0.0);
+            h *= 0.25;
+            if (!(h > 2.220446049250313e-15 * fmax(fabs(t), 1e-300))) return PCK_ST_STEPFAIL;
+            continue;
+        }
+        const double k1 = grp_solve<NSP, G>(x, F, keep * F0);
         double fu = grp_rhs<NSP, G>(gv, x, y + a21 * k1);
-        const double k2 = grp_solve<NSP, G>(x, F, fu + ih * (C21 * k1));
+        const double k2 = grp_solve<NSP, G>(x, F, keep * (fu + ih * (C21 * k1)));
         fu = grp_rhs<NSP, G>(gv, x, y + a31 * k1 + a32 * k2);
-        const double k3 = grp_solve<NSP, G>(x, F, fu + ih * (C31 * k1 + C32 * k2));
+        const double k3 = grp_solve<NSP, G>(x, F, keep * (fu + ih * (C31 * k1 + C32 * k2)));
         fu = grp_rhs<NSP, G>(gv, x, y + a41 * k1 + a42 * k2 + a43 * k3);
-        const double k4 = grp_solve<NSP, G>(x, F, fu + ih * (C41 * k1 + C42 * k2 + C43 * k3));
+        const double k4 = grp_solve<NSP, G>(x, F, keep * (fu + ih * (C41 * k1 + C42 * k2 + C43 * k3)));
         double u = y + a51 * k1 + a52 * k2 + a53 * k3 + a54 * k4;
         fu = grp_rhs<NSP, G>(gv, x, u);
-        const double k5 = grp_solve<NSP, G>(x, F, fu + ih * (C51 * k1 + C52 * k2 + C53 * k3 + C54 * k4));
+        const double k5 = grp_solve<NSP, G>(x, F, keep * (fu + ih * (C51 * k1 + C52 * k2 + C53 * k3 + C54 * k4)));
         u += k5;
         fu = grp_rhs<NSP, G>(gv, x, u);
-        const double k6 = grp_solve<NSP, G>(x, F, fu + ih * (C61 * k1 + C62 * k2 + C63 * k3 + C64 * k4 + C65 * k5));
+        const double k6 = grp_solve<NSP, G>(x, F, keep * (fu + ih * (C61 * k1 + C62 * k2 + C63 * k3 + C64 * k4 +
+                                                                     C65 * k5)));
         u += k6;
         const bool fin_l = !x.row || (isfinite(u) && isfinite(k6));
         const double fin = gmin<G>(fin_l ? 1.0 : 0.0);
@@ -400,11 +462,16 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
         const double r = k6 * __builtin_amdgcn_rcp(sc);     // error weight: the v_rcp_f64 estimate suffices
         const double s = gsum<G>(x.row ? r * r : 0.0);
         const double q = (fin > 0.0) ? s * invNS : INFINITY;     // en^2
+        // positivity (mass-action concentrations stay >= 0): a step that
+        // drives a component below -atol is rejected and retried at the
+        // fraction of the step where that component reaches -atol; accepted
+        // states are clipped at 0, so a component never sits below zero
+        const double pf = gmin<G>((x.row && u < -atol) ? (y + atol) / (y - u) : 1.0);
         const double fac = step_factor(q);
         trace(q, 1.0);
-        if (q <= 1.0) {
+        if (q <= 1.0 && pf >= 1.0) {
             t = last ? t_end : t + h;
-            y = x.row ? u : 0.0;
+            y = x.row ? fmax(u, 0.0) : 0.0;        // tolerance-level negatives (>= -atol) to 0
 #pragma unroll
             for (int l = 0; l < PCK_MAX_CONS; ++l) {
                 if (l < nv.NCONS) {
@@ -417,9 +484,19 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
             }
             F0 = grp_rhs<NSP, G>(gv, x, y);
             h *= fmin(6.0, fmax(0.2, fac));
+        } else if (q <= 1.0) {
+            h *= fmax(0.1, 0.9 * pf);
         } else {
             h *= (fin > 0.0) ? fmax(0.2, fac) : 0.25;
+            // a step whose error is 1e6x the tolerance (or not finite) means
+            // I/(h g) - J was near singular -- the step size sits on an
+            // explosive mode of J; a solve that keeps growing h back into it
+            // cannot advance (scipy BDF stops with "step size less than
+            // spacing" on the same conditions)
+            if (!(q < PCK_BLOWUP_Q) && h < 1e-4 * t && ++blowups > PCK_MAX_BLOWUPS) return PCK_ST_STEPFAIL;
         }
+        stall = (h < PCK_STALL_H * (t - t0)) ? stall + 1 : 0;
+        if (stall > PCK_STALL_STEPS) return PCK_ST_STEPFAIL;
         // scipy's BDF limit: a step below 10 ulp(t) is a failure
         if (!(h > 2.220446049250313e-15 * fmax(fabs(t), 1e-300)) && t < t_end) return PCK_ST_STEPFAIL;
     }
@@ -427,7 +504,7 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
 }
 
 // Newton steady-state polish (same rules as mk_solver.h: newton)
-template <int NSP, int G>
+template <int NSP, int G, int P>
 __device__ __forceinline__ int grp_newton(const NetView& nv, const GrpView& gv, const Grp<NSP>& x, double& y,
                                           int iters) {
     const int NS = x.NS;
@@ -448,7 +525,7 @@ __device__ __forceinline__ int grp_newton(const NetView& nv, const GrpView& gv, 
     LU<NSP> F;
     for (int it = 0; it < iters; ++it) {
         double Gv = grp_rhs<NSP, G>(gv, x, z);
-        grp_jac<NSP, G>(gv, x, z, 1.0, 0.0, F.W);
+        grp_jac<NSP, G, P>(nv, gv, x, z, 1.0, 0.0, F.W);
 #pragma unroll
         for (int l = 0; l < PCK_MAX_CONS; ++l) {
             if (l < nv.NCONS) {
@@ -497,28 +574,24 @@ __device__ __forceinline__ int grp_newton(const NetView& nv, const GrpView& gv, 
 // ---------------------------------------------------------------------------
 // group setup + kernels
 // ---------------------------------------------------------------------------
-__host__ __device__ inline size_t grp_lds_doubles(int R, int NSP, int NS) {
-    return (size_t)2 * (R > 0 ? R : 1) + 4 * (size_t)NSP + (size_t)(NSP + 1) / 2 + (size_t)NS * NS;
-}
-
 template <int NSP, int G>
-__device__ __forceinline__ void grp_setup(const NetView& nv, const CondView& cv, int64_t c, const double* kf,
-                                          const double* kr, int64_t ld_k, int pj, double pfac, double* base,
-                                          Grp<NSP>& x, double& T) {
+__device__ __forceinline__ void grp_setup(const NetView& nv, const GrpView& gv, const CondView& cv, int64_t c,
+                                          const double* kf, const double* kr, int64_t ld_k, int pj, double pfac,
+                                          double* base, int QB, Grp<NSP>& x, double& T) {
     const int R = nv.NRXN;
+    const int r1 = R > 0 ? R : 1;
     x.gl = threadIdx.x % G;
     x.cidx = c;
     x.NS = nv.NDYN;
     x.R = R;
+    x.QB = QB;
     x.row = x.gl < x.NS;
     x.kf = base;
-    x.kr = base + (R > 0 ? R : 1);
-    x.c = x.kr + (R > 0 ? R : 1);
-    x.cf = x.c + NSP;
-    x.f = x.cf + NSP;
-    x.pb = x.f + NSP;
-    x.perm = (int*)(x.pb + NSP);
-    x.J = x.pb + NSP + (NSP + 1) / 2;
+    x.kr = x.kf + grp_even(r1);
+    x.c = x.kr + grp_even(r1);
+    x.d = x.c + grp_even(NSP);
+    x.J = x.d + grp_even(gv.ND > r1 ? gv.ND : r1);
+    x.pb = x.J + grp_even(x.NS * QB);
     T = cv.T[c * cv.sT];
     for (int j = x.gl; j < R; j += G) {
         double a = kf[j * ld_k + c], b = kr[j * ld_k + c];
@@ -534,16 +607,17 @@ __device__ __forceinline__ void grp_setup(const NetView& nv, const CondView& cv,
         x.kf[j] = a;
         x.kr[j] = b;
     }
-    for (int q = 0; q < x.NS; ++q)
-        if (x.row) x.J[q * x.NS + x.gl] = 0.0;
     x.cfi = x.rs = x.fl = x.in = 0.0;
+    x.rb = x.re = 0;
     if (x.row) {
+        for (int j = 0; j < QB; ++j) x.J[x.gl * QB + j] = 0.0;
         const double* d = nv.dyn + 4 * x.gl;
         x.cfi = d[0];
         x.rs = (d[2] != 0.0) ? d[1] + d[2] * T : d[1];   // reactor.py:34-41
         x.fl = d[3];
         if (x.fl != 0.0 && cv.inflow) x.in = cv.inflow[x.gl * cv.ld_in + c * cv.s_in];
-        x.cf[x.gl] = x.cfi;
+        x.rb = gv.row[x.gl];
+        x.re = gv.row[x.gl + 1];
     }
     wsync();
 }
@@ -553,18 +627,22 @@ template <int NSP, int G>
 __device__ __forceinline__ double grp_tof(const NetView& nv, const GrpView& g, const Grp<NSP>& x, double y) {
     put_c(x, y);
     double t = 0.0;
-    for (int k = x.gl; k < nv.NTOF; k += G) t += rec_rate(load_rec(g.rx + nv.tof[k]), x.kf, x.kr, x.c);
+    for (int k = x.gl; k < nv.NTOF; k += G) {
+        const int r = nv.tof[k];
+        t += rec_rate(g.rx[r], x.kf[r], x.kr[r], x.c);
+    }
     return gsum<G>(t);
 }
 
 struct GrpArgs {
     int M;              // groups per condition: 1, or 2R+1 in DRC mode
+    int QB;             // Jacobian column block (= ceil(NSP / P))
     double* tofbuf;     // DRC mode: [M][n] TOF per perturbation
     int32_t* stbuf;     // DRC mode: [M][n] status per perturbation
     int32_t* nsbuf;     // DRC mode: [M][n] integrator steps per perturbation
 };
 
-template <int NSP, int G>
+template <int NSP, int G, int P>
 __global__ void __launch_bounds__(64) k_solve_grp(NetView nv, GrpView gv, CondView cv, const double* kf,
                                                   const double* kr, int64_t ld_k, SolveArgs a, GrpArgs ga) {
     extern __shared__ double lds[];
@@ -578,12 +656,12 @@ __global__ void __launch_bounds__(64) k_solve_grp(NetView nv, GrpView gv, CondVi
     if (q > 0) { pj = (q - 1) >> 1; pfac = (q & 1) ? 1.0 + a.eps : 1.0 - a.eps; }
     Grp<NSP> x;
     double T;
-    grp_setup<NSP, G>(nv, cv, c, kf, kr, ld_k, pj, pfac,
-                      lds + (size_t)grp * grp_lds_doubles(nv.NRXN, NSP, nv.NDYN), x, T);
+    grp_setup<NSP, G>(nv, gv, cv, c, kf, kr, ld_k, pj, pfac,
+                      lds + (size_t)grp * grp_lds_doubles(nv.NRXN, NSP, nv.NDYN, gv.ND, ga.QB), ga.QB, x, T);
     double y = x.row ? cv.y0[x.gl * cv.ld_y0 + c * cv.s_y0] : 0.0;
     int ns = 0;
-    int st = grp_integrate<NSP, G>(nv, gv, x, y, a.t0, a.t_end, a.rtol, a.atol, a.max_steps, ns);
-    if (st == PCK_ST_OK && a.newton) st = grp_newton<NSP, G>(nv, gv, x, y, a.newton_iters);
+    int st = grp_integrate<NSP, G, P>(nv, gv, x, y, a.t0, a.t_end, a.rtol, a.atol, a.max_steps, ns, a.cons_rows != 0);
+    if (st == PCK_ST_OK && a.newton) st = grp_newton<NSP, G, P>(nv, gv, x, y, a.newton_iters);
     const double tof = grp_tof<NSP, G>(nv, gv, x, y);
     const bool fin = gmin<G>((!x.row || isfinite(y)) ? 1.0 : 0.0) > 0.0 && isfinite(tof);
     if (!fin && st == PCK_ST_OK) st = PCK_ST_NONFINITE;
@@ -625,25 +703,25 @@ __global__ void __launch_bounds__(256) k_drc_combine(int64_t n, int R, double ep
     if (nsteps) nsteps[c] = ns;
 }
 
-template <int NSP, int G>
+template <int NSP, int G, int P>
 __global__ void __launch_bounds__(64) k_rates_grp(NetView nv, GrpView gv, CondView cv, const double* kf,
                                                   const double* kr, int64_t ld_k, const double* yin, int64_t ld_y,
-                                                  double* out, int jac) {
+                                                  double* out, int jac, int QB) {
     extern __shared__ double lds[];
     const int grp = threadIdx.x / G;
     const int64_t c = (int64_t)blockIdx.x * (64 / G) + grp;
     if (c >= cv.n) return;
     Grp<NSP> x;
     double T;
-    grp_setup<NSP, G>(nv, cv, c, kf, kr, ld_k, -1, 1.0, lds + (size_t)grp * grp_lds_doubles(nv.NRXN, NSP, nv.NDYN),
-                      x, T);
+    grp_setup<NSP, G>(nv, gv, cv, c, kf, kr, ld_k, -1, 1.0,
+                      lds + (size_t)grp * grp_lds_doubles(nv.NRXN, NSP, nv.NDYN, gv.ND, QB), QB, x, T);
     const double y = x.row ? yin[x.gl * ld_y + c] : 0.0;
     if (!jac) {
         const double f = grp_rhs<NSP, G>(gv, x, y);
         if (x.row) out[x.gl * ld_y + c] = f;
     } else {
         double W[NSP];
-        grp_jac<NSP, G>(gv, x, y, 1.0, 0.0, W);
+        grp_jac<NSP, G, P>(nv, gv, x, y, 1.0, 0.0, W);
         if (x.row) {
 #pragma unroll
             for (int q = 0; q < NSP; ++q)

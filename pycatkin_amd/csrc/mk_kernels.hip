@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 #include <mutex>
 #include <new>
@@ -26,7 +27,7 @@ struct pck_network {
     NetView nv;
     int32_t* d_ip = nullptr;
     double* d_dp = nullptr;
-    GrpRec* d_grx = nullptr;        // lane-group solver (mk_group.h): one record per reaction
+    void* d_grp = nullptr;          // lane-group plan (mk_group.h): reaction records, species CSR of S
     int grp_ok = 0;                 // every reaction fits a record (<= 6 participants, exponents <= 31)
     GrpView gv;
     int spec = 0;                   // id of the compiled-in plan (networks.h) or 0
@@ -34,6 +35,7 @@ struct pck_network {
     unsigned long long digest = 0;
     std::string jit_src;            // mk_jit.h: constexpr plan source for hipRTC (lane networks without a compiled plan)
     bool jit_on = false;            // the last lane solve ran the hipRTC-compiled plan
+    bool grp_jit_on = false;        // the last lane-group solve ran the exact-size hipRTC kernel
 };
 
 // FNV-1a 64 over the solver-side structure (network.py: structural_digest)
@@ -103,6 +105,37 @@ __global__ void __launch_bounds__(64) k_energies(NetView nv, CondView cv, double
 }
 
 #include "mk_solver.h"
+
+// forward / reverse rate of every active reaction at states y, fixed species
+// folded in (System._calc_rates, system.py:345-376; old_system.py:202-225
+// reaction_terms).  One lane per condition; not on the solve path.
+__global__ void __launch_bounds__(64) k_reaction_rates(NetView nv, CondView cv, const double* kf, const double* kr,
+                                                       int64_t ld_k, const double* y, int64_t ld_y, double* rf,
+                                                       double* rr, int64_t ld_r) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= cv.n) return;
+    for (int j = 0; j < nv.NRXN; ++j) {
+        double a = kf[j * ld_k + c], b = kr[j * ld_k + c];
+        for (int q = 0; q < nv.NFIX; ++q) {
+            const int ea = nv.foldf[j * nv.NFIX + q], eb = nv.foldr[j * nv.NFIX + q];
+            if (ea | eb) {
+                const double x = cv.fixc[q * cv.ld_fix + c * cv.s_fix];
+                if (ea) a *= ipow(x, ea);
+                if (eb) b *= ipow(x, eb);
+            }
+        }
+        for (int i = 0; i < nv.NDYN; ++i) {
+            const int ea = nv.expf[j * nv.NDYN + i], eb = nv.expr[j * nv.NDYN + i];
+            if (ea | eb) {
+                const double x = nv.dyn[4 * i] * y[i * ld_y + c];
+                if (ea) a *= ipow(x, ea);
+                if (eb) b *= ipow(x, eb);
+            }
+        }
+        rf[j * ld_r + c] = a;
+        rr[j * ld_r + c] = b;
+    }
+}
 
 // ----------------------------------------------------------------------------
 // C-ABI
@@ -210,52 +243,74 @@ extern "C" int pck_network_create(const int32_t* ip, int64_t n_ip, const double*
     nv.rxd = Dp + doff[PCK_D_RX]; nv.S = Dp + doff[PCK_D_STOICH]; nv.dyn = Dp + doff[PCK_D_DYN];
     nv.C = Dp + doff[PCK_D_CONS];
     net->nv = nv;
-    // sparse plan for the lane-group solver (mk_group.h): one record per
-    // reaction (packed participants) and one per nonzero of S, CSR by species
+    // lane-group plan (mk_group.h): one 16-byte record per reaction (packed
+    // participants + offset of their derivatives) and the species CSR of S
+    // whose entries carry the reaction's participants
     {
         const int R = nv.NRXN, NS = nv.NDYN;
         const double* S = dp + doff[PCK_D_STOICH];
-        std::vector<GrpRec> rx(R > 0 ? R : 1);
-        net->grp_ok = 1;
+        std::vector<uint32_t> rx(4 * (size_t)(R > 0 ? R : 1), 0u);
+        std::vector<int> npv(R > 0 ? R : 1, 0), dpv(R > 0 ? R : 1, 0), spv(6 * (size_t)(R > 0 ? R : 1), 0);
+        net->grp_ok = (R <= 511) ? 1 : 0;
+        int ND = 0;
         for (int j = 0; j < R; ++j) {
-            GrpRec& q = rx[j];
-            memset(&q, 0, sizeof(q));
-            q.r = j;
-            uint32_t w[3] = {0, 0, 0}, sp[3] = {0, 0, 0};
+            uint32_t w[3] = {0, 0, 0};
+            int n = 0;
             for (int i = 0; i < NS; ++i) {
                 const int ea = ip[oef + j * NS + i], eb = ip[oer + j * NS + i];
-                if (ea | eb) {
-                    if (q.np == PCK_GRP_MAX_PART || ea > PCK_GRP_MAX_EXP || eb > PCK_GRP_MAX_EXP) {
-                        net->grp_ok = 0;
-                    } else {
-                        const uint32_t f = (uint32_t)i | ((uint32_t)ea << 6) | ((uint32_t)eb << 11);
-                        w[q.np >> 1] |= f << (16 * (q.np & 1));
-                        ++q.np;
-                    }
+                if (!(ea | eb)) continue;
+                if (n == PCK_GRP_MAX_PART || ea > PCK_GRP_MAX_EXP || eb > PCK_GRP_MAX_EXP) {
+                    net->grp_ok = 0;
+                    continue;
                 }
-                if (S[i * R + j] != 0.0) {
-                    if (q.ns == PCK_GRP_MAX_STOICH) {
-                        net->grp_ok = 0;
-                    } else {
-                        sp[q.ns >> 2] |= (uint32_t)i << (8 * (q.ns & 3));
-                        q.s[q.ns] = S[i * R + j];
-                        ++q.ns;
-                    }
-                }
+                const uint32_t f = (uint32_t)i | ((uint32_t)ea << 6) | ((uint32_t)eb << 11);
+                w[n >> 1] |= f << (16 * (n & 1));
+                spv[6 * j + n] = i;
+                ++n;
             }
-            q.w0 = w[0]; q.w1 = w[1]; q.w2 = w[2];
-            q.sp0 = sp[0]; q.sp1 = sp[1]; q.sp2 = sp[2];
+            npv[j] = n;
+            dpv[j] = ND;
+            ND += n;
+            rx[4 * j + 0] = w[0]; rx[4 * j + 1] = w[1]; rx[4 * j + 2] = w[2];
+            rx[4 * j + 3] = (uint32_t)ND - (uint32_t)n | ((uint32_t)n << 16);
         }
-        GrpRec* drx = nullptr;
-        e = hipMalloc(&drx, sizeof(GrpRec) * rx.size());
-        if (e == hipSuccess) e = hipMemcpy(drx, rx.data(), sizeof(GrpRec) * rx.size(), hipMemcpyHostToDevice);
-        net->d_grx = drx;
+        if (ND > 0x3fff) net->grp_ok = 0;
+        std::vector<int32_t> row(NS + 1, 0);
+        std::vector<uint32_t> ent;
+        for (int i = 0; i < NS; ++i) {
+            row[i] = (int32_t)(ent.size() / 4);
+            for (int j = 0; j < R; ++j) {
+                const double sv = S[i * R + j];
+                if (sv == 0.0) continue;
+                const int n = npv[j];
+                uint32_t a = (uint32_t)j | ((uint32_t)n << 9) | ((uint32_t)dpv[j] << 12);
+                if (n > 5) a |= (uint32_t)spv[6 * j + 5] << 26;
+                uint32_t bb = 0;
+                for (int k = 0; k < n && k < 5; ++k) bb |= (uint32_t)spv[6 * j + k] << (6 * k);
+                uint32_t sw[2];
+                memcpy(sw, &sv, sizeof(sv));
+                ent.push_back(a); ent.push_back(bb); ent.push_back(sw[0]); ent.push_back(sw[1]);
+            }
+        }
+        row[NS] = (int32_t)(ent.size() / 4);
+        if (ent.empty()) ent.assign(4, 0u);
+        const size_t brx = sizeof(uint32_t) * rx.size(), bent = sizeof(uint32_t) * ent.size();
+        const size_t brow = sizeof(int32_t) * row.size();
+        char* buf = nullptr;
+        e = hipMalloc((void**)&buf, brx + bent + brow);
+        if (e == hipSuccess) e = hipMemcpy(buf, rx.data(), brx, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpy(buf + brx, ent.data(), bent, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpy(buf + brx + bent, row.data(), brow, hipMemcpyHostToDevice);
+        net->d_grp = buf;
         if (e != hipSuccess) {
-            (void)hipFree(net->d_ip); (void)hipFree(net->d_dp); (void)hipFree(drx);
+            (void)hipFree(net->d_ip); (void)hipFree(net->d_dp); (void)hipFree(buf);
             delete net;
             return fail(PCK_E_HIP, "HIP error: %s (%lld)", hipGetErrorString(e), (long long)e);
         }
-        net->gv.rx = drx;
+        net->gv.rx = (const uint4*)buf;
+        net->gv.ent = (const uint4*)(buf + brx);
+        net->gv.row = (const int32_t*)(buf + brx + bent);
+        net->gv.ND = ND;
     }
     // structural digest -> compiled-in plan (same bytes as network.py: structural_digest)
     {
@@ -283,7 +338,7 @@ extern "C" int pck_network_create(const int32_t* ip, int64_t n_ip, const double*
 
 extern "C" int pck_network_destroy(pck_network* net) {
     if (!net) return PCK_OK;
-    (void)hipFree(net->d_ip); (void)hipFree(net->d_dp); (void)hipFree(net->d_grx);
+    (void)hipFree(net->d_ip); (void)hipFree(net->d_dp); (void)hipFree(net->d_grp);
     delete net;
     return PCK_OK;
 }
@@ -431,22 +486,39 @@ static bool use_group(const pck_network* net, int lanes_per_cond) {
     return net->plan_mode == PCK_PLAN_GROUP || v.NDYN > PCK_MAX_DYN_LANE || lds_bytes(v.NRXN, v.NDYN, 128) > 64 * 1024 ||
            lanes_per_cond > 64;
 }
-static inline int grp_nsp(int NS) { return NS <= 16 ? 16 : NS <= 32 ? 32 : NS <= 48 ? 48 : 64; }
+// Lane-group kernels: compiled-in sizes <NSP, G, P> (NS <= NSP) and the
+// exact-size specialisation hipRTC compiles at the first solve (mk_jit.h).
 static inline int grp_g(int NS) { return NS <= 16 ? 16 : NS <= 32 ? 32 : 64; }
-#define PCK_GRP_SWITCH(NS, CALL)          \
-    if ((NS) <= 16) { CALL(16, 16); }      \
-    else if ((NS) <= 32) { CALL(32, 32); } \
-    else if ((NS) <= 48) { CALL(48, 64); } \
-    else { CALL(64, 64); }
+// Jacobian column passes: keep the group's J block near 6 KiB of LDS
+static inline int grp_p(int NS) { const int b = NS * NS * 8; return b <= 6144 ? 1 : b <= 12288 ? 2 : 4; }
+#define PCK_GRP_SWITCH(NS, CALL)              \
+    if ((NS) <= 16) { CALL(16, 16, 1); }       \
+    else if ((NS) <= 32) { CALL(32, 32, 2); }  \
+    else { CALL(64, 64, 4); }
+static inline int grp_nsp_ct(int NS) { return NS <= 16 ? 16 : NS <= 32 ? 32 : 64; }
+static inline int grp_p_ct(int NS) { return NS <= 16 ? 1 : NS <= 32 ? 2 : 4; }
+
+static int grp_shape(const pck_network* net, int nsp, int P, size_t* shm, int* QB) {
+    const int NS = net->nv.NDYN;
+    const int per = 64 / grp_g(NS);
+    *QB = (nsp + P - 1) / P;
+    *shm = sizeof(double) * per * grp_lds_doubles(net->nv.NRXN, nsp, NS, net->gv.ND, *QB);
+    if (*shm > 64 * 1024)
+        return fail(PCK_E_SIZE, "lane-group solver: network needs %s%lld bytes of LDS per wavefront", "", (long long)*shm);
+    return PCK_OK;
+}
 
 static int launch_grp_rates(const pck_network* net, const pck_conditions* cond, const double* kf, const double* kr,
                             int64_t ld_k, const double* y, int64_t ld_y, double* out, int jac, hipStream_t s) {
-    if (!net->grp_ok) return fail(PCK_E_SIZE, "lane-group solver: a reaction has more than 6 dynamic participants or stoichiometric species%s", "");
+    if (!net->grp_ok) return fail(PCK_E_SIZE, "lane-group solver: a reaction has more than 6 dynamic participants%s", "");
     const int NS = net->nv.NDYN;
     const int per = 64 / grp_g(NS);
     dim3 g((unsigned)((cond->n + per - 1) / per));
-    const size_t shm = sizeof(double) * per * grp_lds_doubles(net->nv.NRXN, grp_nsp(NS), NS);
-#define CALL(P, GG) hipLaunchKernelGGL((k_rates_grp<P, GG>), g, dim3(64), shm, s, net->nv, net->gv, cview(cond), kf, kr, ld_k, y, ld_y, out, jac)
+    size_t shm;
+    int QB;
+    int rc = grp_shape(net, grp_nsp_ct(NS), grp_p_ct(NS), &shm, &QB);
+    if (rc) return rc;
+#define CALL(NP, GG, PP) hipLaunchKernelGGL((k_rates_grp<NP, GG, PP>), g, dim3(64), shm, s, net->nv, net->gv, cview(cond), kf, kr, ld_k, y, ld_y, out, jac, QB)
     PCK_GRP_SWITCH(NS, CALL)
 #undef CALL
     HIPCHK(hipGetLastError());
@@ -468,6 +540,21 @@ extern "C" int pck_species_rates(const pck_network* net, const pck_conditions* c
 #define CALL(N) hipLaunchKernelGGL(k_species_rates<N>, g, dim3(B), shm, (hipStream_t)stream, net->nv, cview(cond), kf, kr, ld_k, y, ld_y, dydt)
     PCK_NS_SWITCH(net->nv.NDYN, CALL)
 #undef CALL
+    HIPCHK(hipGetLastError());
+    return PCK_OK;
+}
+
+extern "C" int pck_reaction_rates(const pck_network* net, const pck_conditions* cond, const double* kf,
+                                  const double* kr, int64_t ld_k, const double* y, int64_t ld_y, double* rf,
+                                  double* rr, int64_t ld_r, void* stream) {
+    int rc = check_cond(net, cond, true);
+    if (rc) return rc;
+    const int64_t n = cond->n;
+    if (n == 0 || net->nv.NRXN == 0) return PCK_OK;
+    if (!kf || !kr || !y || !rf || !rr || ld_k < n || ld_y < n || ld_r < n)
+        return fail(PCK_E_ARG, "bad state/rate arrays%s", "");
+    hipLaunchKernelGGL(k_reaction_rates, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, (hipStream_t)stream, net->nv,
+                       cview(cond), kf, kr, ld_k, y, ld_y, rf, rr, ld_r);
     HIPCHK(hipGetLastError());
     return PCK_OK;
 }
@@ -515,9 +602,17 @@ static int launch_solve(pck_network* net, const pck_conditions* cond, const pck_
     a.t0 = prm->t0; a.t_end = prm->t_end; a.rtol = prm->rtol; a.atol = prm->atol; a.eps = prm->drc_eps;
     a.max_steps = prm->max_steps; a.newton = prm->newton; a.newton_iters = prm->newton_iters;
     a.want_activity = prm->want_activity;
+    {
+        // conservation rows in the stage systems (mk_solver.h: cons_rows) are
+        // off by default: measured on examples/DMTM at 400 K they cost 1.5x
+        // (GPU) to 2.6x (numpy restatement) more steps -- the pivot species
+        // inherits the cancellation of the other coverages' increments
+        const char* e = getenv("PCK_CONS_ROWS");
+        a.cons_rows = (e && e[0] == '1');
+    }
     if (drc_groups || use_group(net, a.G)) {
         if (!net->grp_ok)
-            return fail(PCK_E_SIZE, "lane-group solver: a reaction has more than 6 dynamic participants or stoichiometric species%s", "");
+            return fail(PCK_E_SIZE, "lane-group solver: a reaction has more than 6 dynamic participants%s", "");
         GrpArgs ga;
         ga.M = drc_groups ? drc_groups : 1;
         ga.tofbuf = nullptr;
@@ -533,13 +628,33 @@ static int launch_solve(pck_network* net, const pck_conditions* cond, const pck_
             ga.nsbuf = ga.stbuf + m;
         }
         const int NS = net->nv.NDYN;
-        const int per = 64 / grp_g(NS);
+        const int G = grp_g(NS);
+        const int per = 64 / G;
         const int64_t groups = n * ga.M;
         dim3 g((unsigned)((groups + per - 1) / per));
-        const size_t shm = sizeof(double) * per * grp_lds_doubles(R, grp_nsp(NS), NS);
-#define CALL(P, GG) hipLaunchKernelGGL((k_solve_grp<P, GG>), g, dim3(64), shm, s, net->nv, net->gv, cview(cond), kf, kr, n, a, ga)
-        PCK_GRP_SWITCH(NS, CALL)
+        hipFunction_t f = nullptr;
+        int P = grp_p(NS);
+        if (net->plan_mode != PCK_PLAN_RUNTIME && jit_enabled()) f = jit_group_kernel(NS, G, P);
+        size_t shm;
+        if (f) {
+            rc = grp_shape(net, NS, P, &shm, &ga.QB);
+            if (rc) return rc;
+            NetView nv = net->nv;
+            GrpView gv = net->gv;
+            CondView cv = cview(cond);
+            const double* kfp = kf;
+            const double* krp = kr;
+            int64_t ldk = n;
+            void* args[] = {&nv, &gv, &cv, &kfp, &krp, &ldk, &a, &ga};
+            HIPCHK(hipModuleLaunchKernel(f, g.x, 1, 1, 64, 1, 1, (unsigned)shm, s, args, nullptr));
+        } else {
+            rc = grp_shape(net, grp_nsp_ct(NS), grp_p_ct(NS), &shm, &ga.QB);
+            if (rc) return rc;
+#define CALL(NP, GG, PP) hipLaunchKernelGGL((k_solve_grp<NP, GG, PP>), g, dim3(64), shm, s, net->nv, net->gv, cview(cond), kf, kr, n, a, ga)
+            PCK_GRP_SWITCH(NS, CALL)
 #undef CALL
+        }
+        net->grp_jit_on = (f != nullptr);
         HIPCHK(hipGetLastError());
         if (drc_groups) {
             hipLaunchKernelGGL(k_drc_combine, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, R, a.eps,

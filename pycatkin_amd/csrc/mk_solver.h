@@ -218,11 +218,60 @@ __device__ __forceinline__ void load_keff(const P& p, const NetView& nv, const C
     });
 }
 
+// Conservation rows in the stage system.  With site balances C f(y) = 0
+// for every y, so C J = 0: the iteration matrix I/(h g) - J loses rank as h
+// grows (t_end = 1e12 s in examples/DMTM) and its LU's error lands in the
+// conserved directions.  The exact stage vectors satisfy C k_i = 0, so the
+// pivot row of each law is replaced by that law (scaled to the row's size)
+// and its right-hand side entry by 0: the same solution in exact
+// arithmetic, a well-conditioned system at any h.
+template <class P, int NS>
+__device__ __forceinline__ void cons_rows(const P& p, double (&W)[NS][NS]) {
+    for (int l = 0; l < p.ncons(); ++l) {
+        const int pv = p.cpiv(l);
+#pragma unroll
+        for (int i = 0; i < NS; ++i) {
+            if (i != pv) continue;
+            double m = 0.0;
+#pragma unroll
+            for (int q = 0; q < NS; ++q) m = fmax(m, fabs(W[i][q]));
+#pragma unroll
+            for (int q = 0; q < NS; ++q) W[i][q] = p.C(l, q) * m;
+        }
+    }
+}
+template <class P, int NS>
+__device__ __forceinline__ void cons_zero(const P& p, double (&b)[NS]) {
+    for (int l = 0; l < p.ncons(); ++l) {
+        const int pv = p.cpiv(l);
+#pragma unroll
+        for (int i = 0; i < NS; ++i)
+            if (i == pv) b[i] = 0.0;
+    }
+}
+
 // ---------------------------------------------------------------------------
 // RODAS4 (Hairer & Wanner, stiffly accurate 4(3) Rosenbrock, L-stable),
 // autonomous form:  (I/(h g) - J) k_i = f(u_i) + sum_j C_ij k_j / h,
 // u_{i+1} = y + sum_j a_ij k_j,  y_new = u_5 + k5 + k6,  error = k6.
 // ---------------------------------------------------------------------------
+// A rejected step with en^2 above PCK_BLOWUP_Q (error 1e6 x the tolerance)
+// at a step size below 1e-4 t is catastrophic; more than PCK_MAX_BLOWUPS of
+// them end the solve with PCK_ST_STEPFAIL (a healthy solve has a handful,
+// while its first step size is being found; large-h rejections late in a
+// long run, where I/(h g) - J loses rank along the site balances, do not
+// count).
+#define PCK_BLOWUP_Q 1e12
+#define PCK_MAX_BLOWUPS 200
+// Stagnation: more than PCK_STALL_STEPS consecutive steps with h below
+// PCK_STALL_H * (t - t0) end the solve with PCK_ST_STEPFAIL.  The stalled
+// solves of the synthetic network sit at h ~ 1e-6 t (scipy BDF fails on the
+// same conditions); the slowest healthy solve measured (examples/DMTM at
+// 400 K to 1e12 s at rtol 1e-10 / atol 1e-14, rounding-limited late in the
+// run) keeps h above 2e-5 t.
+#define PCK_STALL_STEPS 16384
+#define PCK_STALL_H 1e-5
+
 namespace rodas4 {
 constexpr double g = 0.25;
 constexpr double a21 = 1.544, a31 = 0.9466785280815826, a32 = 0.2557011698983284;
@@ -239,7 +288,7 @@ constexpr double C61 = 8.083246795921522, C62 = -7.981132988064893, C63 = -31.52
 
 template <class P, class K>
 __device__ int integrate(const P& p, const Lane<P::NS>& L, const K& k, double (&y)[P::NS], double t0,
-                         double t_end, double rtol, double atol, int max_steps, int& nsteps) {
+                         double t_end, double rtol, double atol, int max_steps, int& nsteps, bool crows) {
     using namespace rodas4;
     constexpr int NS = P::NS;
     nsteps = 0;
@@ -286,6 +335,8 @@ __device__ int integrate(const P& p, const Lane<P::NS>& L, const K& k, double (&
     double W[NS][NS];
     int piv[NS];
     unsigned sw;
+    int blowups = 0;
+    int stall = 0;
     while (t < t_end) {
         if (nsteps >= max_steps) return PCK_ST_MAXSTEPS;
         ++nsteps;
@@ -300,35 +351,45 @@ __device__ int integrate(const P& p, const Lane<P::NS>& L, const K& k, double (&
             for (int q = 0; q < NS; ++q) W[i][q] = -W[i][q];
             W[i][i] += ig;
         }
-        if (!lu<NS>(W, piv, sw)) { h *= 0.25; continue; }
+        if (crows) cons_rows(p, W);
+        if (!lu<NS>(W, piv, sw)) {
+            h *= 0.25;
+            if (!(h > 2.220446049250313e-15 * fmax(fabs(t), 1e-300))) return PCK_ST_STEPFAIL;
+            continue;
+        }
         double k1[NS], k2[NS], k3[NS], k4[NS], k5[NS], u[NS], fu[NS];
 #pragma unroll
         for (int i = 0; i < NS; ++i) k1[i] = F0[i];
-        lu_solve<NS>(W, piv, sw,k1);
+        if (crows) cons_zero(p, k1);
+        lu_solve<NS>(W, piv, sw, k1);
 #pragma unroll
         for (int i = 0; i < NS; ++i) u[i] = y[i] + a21 * k1[i];
         rhs(p, L, k, u, fu);
 #pragma unroll
         for (int i = 0; i < NS; ++i) k2[i] = fu[i] + ih * (C21 * k1[i]);
-        lu_solve<NS>(W, piv, sw,k2);
+        if (crows) cons_zero(p, k2);
+        lu_solve<NS>(W, piv, sw, k2);
 #pragma unroll
         for (int i = 0; i < NS; ++i) u[i] = y[i] + a31 * k1[i] + a32 * k2[i];
         rhs(p, L, k, u, fu);
 #pragma unroll
         for (int i = 0; i < NS; ++i) k3[i] = fu[i] + ih * (C31 * k1[i] + C32 * k2[i]);
-        lu_solve<NS>(W, piv, sw,k3);
+        if (crows) cons_zero(p, k3);
+        lu_solve<NS>(W, piv, sw, k3);
 #pragma unroll
         for (int i = 0; i < NS; ++i) u[i] = y[i] + a41 * k1[i] + a42 * k2[i] + a43 * k3[i];
         rhs(p, L, k, u, fu);
 #pragma unroll
         for (int i = 0; i < NS; ++i) k4[i] = fu[i] + ih * (C41 * k1[i] + C42 * k2[i] + C43 * k3[i]);
-        lu_solve<NS>(W, piv, sw,k4);
+        if (crows) cons_zero(p, k4);
+        lu_solve<NS>(W, piv, sw, k4);
 #pragma unroll
         for (int i = 0; i < NS; ++i) u[i] = y[i] + a51 * k1[i] + a52 * k2[i] + a53 * k3[i] + a54 * k4[i];
         rhs(p, L, k, u, fu);
 #pragma unroll
         for (int i = 0; i < NS; ++i) k5[i] = fu[i] + ih * (C51 * k1[i] + C52 * k2[i] + C53 * k3[i] + C54 * k4[i]);
-        lu_solve<NS>(W, piv, sw,k5);
+        if (crows) cons_zero(p, k5);
+        lu_solve<NS>(W, piv, sw, k5);
 #pragma unroll
         for (int i = 0; i < NS; ++i) u[i] += k5[i];
         rhs(p, L, k, u, fu);
@@ -336,7 +397,8 @@ __device__ int integrate(const P& p, const Lane<P::NS>& L, const K& k, double (&
 #pragma unroll
         for (int i = 0; i < NS; ++i)
             k5[i] = fu[i] + ih * (C61 * k1[i] + C62 * k2[i] + C63 * k3[i] + C64 * k4[i] + C65 * k5[i]);
-        lu_solve<NS>(W, piv, sw,k5);
+        if (crows) cons_zero(p, k5);
+        lu_solve<NS>(W, piv, sw, k5);
         bool finite = true;
         double s = 0.0;
 #pragma unroll
@@ -348,11 +410,24 @@ __device__ int integrate(const P& p, const Lane<P::NS>& L, const K& k, double (&
             s += r * r;
         }
         const double q = finite ? s * (1.0 / NS) : INFINITY;    // en^2
+        // positivity (mass-action concentrations stay >= 0): a step that
+        // drives a component below -atol is rejected and retried at the
+        // fraction of the step where that component reaches -atol; accepted
+        // states are clipped at 0, so a component never sits below zero
+        bool negv = false;
+#pragma unroll
+        for (int i = 0; i < NS; ++i) negv = negv || (u[i] < -atol);
+        double pf = 1.0;
+        if (__any(negv)) {          // rare: one wave-uniform branch
+#pragma unroll
+            for (int i = 0; i < NS; ++i)
+                if (u[i] < -atol) pf = fmin(pf, (y[i] + atol) / (y[i] - u[i]));
+        }
         const double fac = step_factor(q);
-        if (q <= 1.0) {
+        if (q <= 1.0 && pf >= 1.0) {
             t = last ? t_end : t + h;
 #pragma unroll
-            for (int i = 0; i < NS; ++i) y[i] = u[i];
+            for (int i = 0; i < NS; ++i) y[i] = fmax(u[i], 0.0);     // tolerance-level negatives (>= -atol) to 0
             // Rosenbrock stages keep linear invariants only up to the rounding of
             // the stiff LU; rescale each non-negative site balance back onto its
             // initial total (multiplicative, so tiny coverages keep their digits)
@@ -373,9 +448,15 @@ __device__ int integrate(const P& p, const Lane<P::NS>& L, const K& k, double (&
             }
             rhs(p, L, k, y, F0);
             h *= fmin(6.0, fmax(0.2, fac));
+        } else if (q <= 1.0) {
+            h *= fmax(0.1, 0.9 * pf);
         } else {
             h *= finite ? fmax(0.2, fac) : 0.25;
+            // repeated catastrophic rejections: see mk_group.h grp_integrate
+            if (!(q < PCK_BLOWUP_Q) && h < 1e-4 * t && ++blowups > PCK_MAX_BLOWUPS) return PCK_ST_STEPFAIL;
         }
+        stall = (h < PCK_STALL_H * (t - t0)) ? stall + 1 : 0;
+        if (stall > PCK_STALL_STEPS) return PCK_ST_STEPFAIL;
         // scipy's BDF limit: a step below 10 ulp(t) is a failure
         if (!(h > 2.220446049250313e-15 * fmax(fabs(t), 1e-300)) && t < t_end) return PCK_ST_STEPFAIL;
     }
@@ -553,6 +634,7 @@ struct SolveArgs {
     double* tof; int32_t* status; int32_t* nsteps;
     double* xi; int64_t ld_xi; double* tof0;   // DRC mode
     int G;                                     // lanes per condition (1, or DRC group size)
+    int cons_rows;                             // conservation rows in the stage systems (A/B: PCK_CONS_ROWS=0)
 };
 
 template <class P>
@@ -610,7 +692,7 @@ __global__ void __launch_bounds__(PCK_SOLVE_BLOCK) __attribute__((amdgpu_waves_p
         double y[NS];
 #pragma unroll
         for (int i = 0; i < NS; ++i) y[i] = cv.y0[i * cv.ld_y0 + c * cv.s_y0];
-        st = integrate(p, L, k, y, a.t0, a.t_end, a.rtol, a.atol, a.max_steps, ns);
+        st = integrate(p, L, k, y, a.t0, a.t_end, a.rtol, a.atol, a.max_steps, ns, a.cons_rows != 0);
         if (st == PCK_ST_OK && a.newton) st = newton(p, L, k, y, a.newton_iters);
         tof = lane_tof(p, nv, k, y);
         bool fin = isfinite(tof);

@@ -146,6 +146,18 @@ class DeviceNetwork:
                                            _ptr(out), _stream(torch)))
         return out
 
+    def reaction_rates(self, n, T, p, y, kf, kr, desc=None, fixc=None):
+        """pck_reaction_rates: (rf, rr) [NRXN, n] at states y [NDYN, n]."""
+        torch = self.torch
+        c, keep = self.conditions(n, T, p, desc, fixc, None, None)
+        y = torch.as_tensor(y, dtype=torch.float64, device='cuda').reshape(self.NDYN, n).contiguous()
+        kf, kr = kf.contiguous(), kr.contiguous()
+        rf = torch.empty((max(self.NRXN, 1), n), dtype=torch.float64, device='cuda')
+        rr = torch.empty_like(rf)
+        L.check(self.lib.pck_reaction_rates(self.h, C.byref(c), _ptr(kf), _ptr(kr), kf.shape[1], _ptr(y), n, _ptr(rf),
+                                            _ptr(rr), n, _stream(torch)))
+        return rf[:self.NRXN], rr[:self.NRXN]
+
     def jacobian(self, n, T, p, y, kf, kr, desc=None, fixc=None, inflow=None):
         torch = self.torch
         c, keep = self.conditions(n, T, p, desc, fixc, None, inflow)

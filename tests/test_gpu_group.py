@@ -306,3 +306,153 @@ def test_synthetic_steady_vs_oracle(P, synthetic):
             assert abs(r['tof'][c] - tof) <= 1e-6 * abs(tof) + 1e-12
         else:   # two integrators' transients on a slow manifold: bounded by their error
             assert close(r['y'][:, c], yT[dyn], rtol=1e-3, floor=1e-9), (c, np.abs(r['y'][:, c] - yT[dyn]).max())
+
+
+def test_group_exact_size_kernel_matches_compiled(P, inputs, monkeypatch):
+    """The lane-group solver hipRTC specialises for the network's exact size
+    (k_solve_grp<11, 16, 1> for DMTM) and the compiled-in padded kernel
+    (k_solve_grp<16, 16, 1>, PCK_JIT=0) do the same arithmetic in the same
+    order: bitwise-equal states, TOFs and step counts.  Two runs of the same
+    launch are bitwise equal too (no cross-lane atomics in the sums)."""
+    s = _dmtm(P, inputs)
+    T = np.linspace(400.0, 800.0, 64)
+    kw = dict(T=T, tof_terms=('r5', 'r9'), steady=True)
+    a = s.solve_batch(**kw)
+    b = s.solve_batch(**kw)
+    monkeypatch.setenv('PCK_JIT', '0')
+    c = s.solve_batch(**kw)
+    monkeypatch.delenv('PCK_JIT')
+    for k in ('y', 'tof', 'status', 'nsteps'):
+        np.testing.assert_array_equal(a[k], b[k])
+        np.testing.assert_array_equal(a[k], c[k])
+    assert np.all(a['status'] == 0)
+
+
+def test_dmtm_pressure_sweep_vs_oracle(P, inputs):
+    """BASELINE configs[3] pressure axis: run_parameters(..., 'pressure') at
+    3 pressures x 3 temperatures, each condition with its own pressure in the
+    gas free energies (state.py:329-331), steady state vs the oracle at 1e-6."""
+    from pycatkin_amd.functions.presets import run_parameters
+    spec = O.load_spec(os.path.join(inputs, 'DMTM', 'input.json'))
+    for T in (450.0, 600.0, 750.0):
+        s = _dmtm(P, inputs)
+        s.params['temperature'] = T
+        ps = np.array([1.0e4, 1.0e5, 1.0e6])
+        final, rates, _ = run_parameters(s, ps, 'pressure', steady_state_solve=True)
+        plan = s.plan()
+        for k, p in enumerate(ps):
+            m = O.ClassicModel(spec, T=T, p=p)
+            yT, _ = m.solve_odes(rtol=1e-10, atol=1e-14)
+            ys = m.find_steady(yT)
+            assert m.regular
+            got = np.array([final[k, plan.species.index(n)] for n in plan.dyn])
+            ref = np.array([ys[m.idx[n]] for n in plan.dyn])
+            assert close(got, ref), (T, p, got, ref)
+            # rates_vs_pressure: r_fwd - r_rev of every reaction at the steady state
+            rr = m.rates(ys)
+            np.testing.assert_allclose(rates[k], rr[:, 0] - rr[:, 1], rtol=1e-6, atol=1e-12 * np.abs(rr).max())
+        # the pressure really enters: the three steady states differ
+        assert np.abs(final[0] - final[2]).max() > 1e-6
+
+
+def _six_species_net():
+    """A 12-species network whose reaction R0 has 6 dynamic participants and
+    6 stoichiometric entries (the widest record of the lane-group plan)."""
+    from pycatkin_amd.functions.synthetic import synthetic_network
+    net = synthetic_network(n_species=12, n_reactions=24, seed=3)
+    ads = net['adsorbates']
+    net['reactions'][10] = ('surf', [ads[0], ads[1], ads[2]], [ads[3], ads[4], ads[5]])
+    return net
+
+
+def test_group_six_participant_reaction_vs_oracle(P):
+    """Rates and Jacobian of a reaction with 6 participants / 6 stoichiometric
+    species on the lane-group path (packed records, mk_group.h) vs the oracle."""
+    from _synth import spec_of
+    from pycatkin_amd.functions.synthetic import synthetic_system
+    net = _six_species_net()
+    sim, _ = synthetic_system(net)
+    plan = sim.plan()
+    dnet = sim.device()
+    assert dnet.NDYN == 12
+    rng = np.random.default_rng(5)
+    n = 5
+    D = rng.uniform(-0.3, 0.3, (4, n))
+    T = np.linspace(480.0, 560.0, n)
+    y = rng.uniform(0.01, 0.2, (12, n))
+    desc = {'D%d' % k: D[k] for k in range(4)}
+    Tt, p, d, fx, y0, inflow = sim._inputs(dnet, plan, n, T, None, desc, None, None, None)
+    kf, kr = dnet.rate_constants(n, Tt, p, d)
+    f = dnet.species_rates(n, Tt, p, y, kf, kr, d, fx, inflow).cpu().numpy()
+    J = dnet.jacobian(n, Tt, p, y, kf, kr, d, fx, inflow).cpu().numpy()
+    for c in range(n):
+        m = O.ClassicModel(spec_of(net, D[:, c], T[c]), T=T[c])
+        full = m.y0.copy()
+        dyn = [m.idx[nm] for nm in plan.dyn]
+        full[dyn] = y[:, c]
+        fr, Jr = m.rhs(full)[dyn], m.jac(full)[np.ix_(dyn, dyn)]
+        np.testing.assert_allclose(f[:, c], fr, rtol=1e-10, atol=1e-12 * np.abs(fr).max())
+        np.testing.assert_allclose(J[:, :, c], Jr, rtol=1e-10, atol=1e-12 * np.abs(Jr).max())
+
+
+def test_ch4_patched_api_vs_oracle(P, inputs):
+    """The patched System's per-call API on the device (system.py:345-564):
+    _calc_rates, get_dydt (every tracked species, gas rows included),
+    _fun_ss, _jac_ss and the surface columns of get_jacobian, vs the oracle's
+    PatchedModel at a random composition."""
+    s, spec = _ch4(P, inputs)
+    s.T = 523.0
+    s.build()
+    m = O.PatchedModel(spec, T=523.0)
+    names = sorted(m.index, key=m.index.get)
+    assert names == sorted(s.index_map, key=s.index_map.get)
+    np.testing.assert_allclose(s.initial_system, m.y0, rtol=1e-15)
+    rng = np.random.default_rng(7)
+    y = m.normalize(rng.uniform(0.01, 1.0, len(names)))
+    np.testing.assert_allclose(s.get_dydt(y), m.dydt(y), rtol=1e-10, atol=1e-12 * np.abs(m.dydt(y)).max())
+    ys = y[m.ngas:]
+    fr, Jr = m.fun_ss(ys), m.jac_ss(ys)
+    np.testing.assert_allclose(s._fun_ss(ys), fr, rtol=1e-10, atol=1e-12 * np.abs(fr).max())
+    np.testing.assert_allclose(s._jac_ss(ys), Jr, rtol=1e-10, atol=1e-12 * np.abs(Jr).max())
+    Jf = s.get_jacobian(y)
+    Jo = m.jacobian(y)
+    np.testing.assert_allclose(Jf[:, m.ngas:], Jo[:, m.ngas:], rtol=1e-10, atol=1e-12 * np.abs(Jo).max())
+    rates = s._calc_rates(y)
+    assert rates.shape == (len(s.rate_map), 2)
+    np.testing.assert_allclose(s.reaction_matrix @ (rates[:, 0] - rates[:, 1]), m.dydt(y), rtol=1e-10,
+                               atol=1e-12 * np.abs(m.dydt(y)).max())
+
+
+def test_ch4_steady_state_solver(P, inputs):
+    """BASELINE configs[0] on the drop-in: SteadyStateSolver(system).solve_ode()
+    (solver.py:374-418: transient from the normalised start state to 1e4 s at
+    rtol 1e-10 / atol 1e-12, then test_convergence), against the oracle's
+    scipy BDF run of the same path at 1e-6.  The patched +-1 formulation does
+    not conserve its site groups and never settles (the oracle's max|f| stays
+    ~1e-4 out to 1e8 s and BDF blows up by 1e10 s), so solve_root's device
+    Newton root is pinned by the oracle's own equations: fun_ss of the
+    oracle vanishes there and the network's linear invariants keep their
+    start values.  The batched solve_ode over temperatures equals single calls."""
+    s, spec = _ch4(P, inputs, 1.0, 1.0)
+    s.T = 523.0
+    solver = P.SteadyStateSolver(s, ss_guess=None)
+    res = solver.solve_ode(tmax=1e4)
+    m = O.PatchedModel(spec, T=523.0)
+    yT, sol = m.solve_ode(tmax=1e4, rtol=1e-10, atol=1e-12, method='BDF')
+    assert sol.status == 0
+    assert close(res.x, yT, rtol=1e-6, floor=1e-12), np.abs(res.x - yT).max()
+    assert res.success == solver.test_convergence(yT)
+    solver2 = P.SteadyStateSolver(s, ss_guess=yT)
+    x, st = solver2._newton(solver2._norm(yT), 30)
+    assert st == 0, st
+    scale = np.abs(m.fun_ss(yT)).max() + np.abs(m.jac_ss(yT)).max() * 1e-12
+    assert np.abs(m.fun_ss(x)).max() <= 1e-6 * scale + 1e-12, np.abs(m.fun_ss(x)).max()
+    C = np.array(s.plan().conservation)
+    if C.size:
+        xp, yp = s._to_plan(s.plan(), x[:, None])[:, 0], s._to_plan(s.plan(), solver2._norm(yT)[:, None])[:, 0]
+        np.testing.assert_allclose(C @ xp, C @ yp, rtol=1e-10, atol=1e-14)
+    r2 = solver2.solve_root()
+    assert r2.success == solver2.test_convergence(r2.x)
+    Y, ok = solver.solve_ode_batch(T=[473.0, 523.0, 573.0])
+    assert ok[1] == res.success
+    np.testing.assert_allclose(Y[:, 1], res.x, rtol=1e-12, atol=1e-300)

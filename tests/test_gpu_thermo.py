@@ -1,0 +1,96 @@
+"""State thermochemistry on the device (kernel 1's energy program, through
+pck_energies) against the reference's own per-state checks in
+test/tests.py:46-58,134-157: the electronic energy from the scaling
+coefficients, the ZPE and the harmonic (Helmholtz) free energy of the
+scaling states, restated with ASE's published HarmonicThermo formulas
+(ASE is not importable here):
+
+    ZPE = 1/2 sum eps,   F = E + ZPE + kB T sum ln(1 - exp(-eps / kB T)),
+    eps = invcm * nu[cm^-1],  ASE's CODATA-2014 constants.
+
+tests.py asserts ceil-rounded equality at 6 / 3 / 3 decimals (its my_round);
+the same assertions hold here, and the values agree to the 1e-4 eV the two
+constant sets differ by.  The O2 gas free energy (tests.py:105-117 only
+prints it) is checked against IdealGasThermo's linear-molecule Gibbs energy
+without its electronic-spin term kB T ln(2S+1), which PyCatKin does not
+include (state.py:320-365)."""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+# ase.units (CODATA 2014)
+KB = 8.617330337e-05                    # eV/K
+INVCM = 1.2398419739640718e-04           # eV per cm^-1
+AMU = 1.66053904e-27
+HPL_EV = 4.135667662e-15                 # eV s
+EV = 1.6021766208e-19
+
+EC, EO = 1.5, 0.2
+STATES = {   # test/tests.py:46-51, 134-157: (coefficients for [EC, EO, 1], frequencies in cm^-1)
+    'sCO': ([0.45, 0, 0.51], [2040.0, 306.9, 268.2, 261.1, 99.7, 68.7]),
+    'sC-H--OH': ([0.89, 0.46, 0.29], [3705.1, 1298.0, 1012.1, 688.3, 613.0, 435.1, 420.5, 358.6, 310.2, 215.0,
+                                      12.2]),
+    'sCH3': ([0.239785047, 0, 0.136587444], [95.8, 103.5, 226.0, 278.8, 545.5, 547.6, 1166.3, 1400.4, 1403.8,
+                                              2944.3, 3014.7, 3016.4]),
+    'sCH2-H': ([0.618905821, 0, 0.19638489], [3080.5, 3007.1, 1406.2, 1361.2, 822.3, 622.7, 534.5, 442.3, 340.2,
+                                               222.8, 77.0]),
+    'sCH2': ([0.494635, 0, 0.232988], [152.0, 257.5, 305.9, 416.3, 434.8, 643.3, 1329.9, 2947.9, 3008.0]),
+    'hH': ([0.219820574, 0, -0.785276035], [978.2, 768.0, 764.8]),
+}
+
+
+def my_round(n, n_dec=4):
+    """test/tests.py:65-66"""
+    return np.ceil(n * 10 ** n_dec) / 10 ** n_dec
+
+
+@pytest.fixture(scope='module')
+def ch4(inputs):
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip('no HIP device')
+    import pycatkin_amd as P
+    s = P.read_from_input_file(os.path.join(inputs, 'CH4', 'input.json'), formulation='patched')
+    s.reactions['C_ads'].dErxn_user = EC
+    s.reactions['O_ads'].dErxn_user = EO
+    s.states['sC'].Gelec = EC
+    s.states['sO'].Gelec = EO
+    return s
+
+
+@pytest.mark.parametrize('name', sorted(STATES))
+def test_scaling_state_energies_vs_harmonic_thermo(ch4, name):
+    coeff, vib_cm = STATES[name]
+    T, p = float(ch4.T), float(ch4.p)
+    st = ch4.states[name]
+    eps = INVCM * np.array(vib_cm)
+    E_pred = float(np.dot(coeff, [EC, EO, 1.0]))
+    zpe = 0.5 * eps.sum()
+    A_pred = E_pred + zpe + KB * T * np.sum(np.log(1.0 - np.exp(-eps / (KB * T))))
+    Gelec = st.get_potential_energy()
+    st.calc_zpe()
+    Gfree = st.get_free_energy(T, p)                       # device: kernel 1 energy program
+    assert my_round(E_pred, 6) == my_round(Gelec, 6)       # tests.py:100
+    assert my_round(zpe, 3) == my_round(st.Gzpe, 3)        # tests.py:101
+    assert my_round(A_pred, 3) == my_round(Gfree, 3)       # tests.py:102
+    assert abs(Gfree - A_pred) < 2e-4, (Gfree, A_pred)
+
+
+def test_o2_gas_free_energy_vs_ideal_gas_thermo(ch4):
+    T, p = float(ch4.T), float(ch4.p)
+    mass, sigma, inertia, E, vib = 31.998, 2, 12.418474628311035, 5.48, [1543.5]   # tests.py:53-59
+    kT = KB * T
+    eps = INVCM * np.array(vib)
+    m = mass * AMU
+    h = HPL_EV * EV                                        # J s
+    kTJ = kT * EV
+    I = inertia * AMU * 1e-20                              # amu A^2 -> kg m^2
+    g_trans = -kT * np.log((2 * np.pi * m * kTJ / h ** 2) ** 1.5 * kTJ / p)
+    g_rot = -kT * np.log(8 * np.pi ** 2 * I * kTJ / (sigma * h ** 2))
+    g_vib = 0.5 * eps.sum() + kT * np.sum(np.log(1.0 - np.exp(-eps / kT)))
+    G_ase_no_spin = E + g_vib + g_trans + g_rot
+    G = ch4.states['O2'].get_free_energy(T, p)
+    assert abs(G - G_ase_no_spin) < 2e-3, (G, G_ase_no_spin)

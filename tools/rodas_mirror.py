@@ -127,13 +127,25 @@ def rodas4(f, J, y, t0, t_end, rtol, atol, cons=None, max_steps=200000, cons_row
         fin = np.all(np.isfinite(unew))
         scl = atol + rtol * np.maximum(np.abs(y), np.abs(unew))
         q = np.mean((ks[5] / scl) ** 2) if fin else np.inf
-        fac = 0.9 * q ** -0.25 if q > 0 else np.inf
-        acc = q <= 1.0
+        fac = 0.9 * q ** -0.125 if q > 0 else np.inf
+        neg = (unew < -atol) & (os.environ.get('NOPOS') is None)
+        pf = float(np.min((y[neg] + atol) / (y[neg] - unew[neg]))) if np.any(neg) else 1.0
+        acc = q <= 1.0 and pf >= 1.0
+        if q <= 1.0 and pf < 1.0:
+            if trace is not None:
+                trace.append((t, h, q, False))
+            h *= max(0.1, 0.9 * pf)
+            continue
         if trace is not None:
             trace.append((t, h, q, acc))
+            if os.environ.get('ERRDUMP') and t > float(os.environ['ERRDUMP']) and len(trace) % 50 == 0:
+                e = ks[5] / scl
+                j = int(np.argmax(np.abs(e)))
+                print('t %.3e h %.3e q %.3e worst comp %d y %.3e unew %.3e e %.3e |e| sorted %s' % (
+                    t, h, q, j, y[j], unew[j], e[j], np.array2string(np.sort(np.abs(e))[::-1][:4], precision=2)))
         if acc:
             t = t_end if last else t + h
-            y = unew
+            y = unew if os.environ.get('NOCLIP') else np.maximum(unew, 0.0)
             if cons is not None:
                 for l in range(cons.shape[0]):
                     if np.all(cons[l] >= 0):
@@ -159,10 +171,23 @@ def synthetic_model(idx, n_total=16384):
     return m, D
 
 
+def dmtm_model(T):
+    from oracle import mk_oracle as O
+    spec = O.load_spec(os.path.join(ROOT, 'tests', 'golden', 'inputs', 'DMTM', 'input.json'))
+    return O.ClassicModel(spec, T=T), [T]
+
+
 def main():
-    which, idx = sys.argv[1], int(sys.argv[2])
-    assert which == 'synthetic'
-    m, D = synthetic_model(idx)
+    which = sys.argv[1]
+    if which == 'dmtm':
+        m, D = dmtm_model(float(sys.argv[2]))
+        D = np.array(D)
+        idx = 0
+        t_end, rtol, atol = 1e12, float(os.environ.get('RTOL', 1e-10)), float(os.environ.get('ATOL', 1e-14))
+    else:
+        idx = int(sys.argv[2])
+        m, D = synthetic_model(idx)
+        t_end, rtol, atol = 1e4, 1e-8, 1e-10
     dyn = m.dyn
     full = m.y0.copy()
 
@@ -179,7 +204,7 @@ def main():
     Cr, piv = _rref(C)
     mode = sys.argv[3] if len(sys.argv) > 3 else 'plain'
     tr = []
-    y, st, n = rodas4(f, J, y0, 0.0, 1e4, 1e-8, 1e-10, cons=Cr, max_steps=int(os.environ.get('MAXSTEPS', 20000)),
+    y, st, n = rodas4(f, J, y0, 0.0, t_end, rtol, atol, cons=Cr, max_steps=int(os.environ.get('MAXSTEPS', 20000)),
                       cons_rows=(Cr, piv) if mode == 'rows' else None, trace=tr, gpu_lu='gpulu' in sys.argv)
     if PIVLOG:
         pl = np.array(PIVLOG)
