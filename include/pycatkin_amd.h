@@ -141,6 +141,8 @@ typedef struct {
     int32_t newton_iters;  /* max Newton iterations */
     int32_t want_activity; /* 1: write activity (eV) instead of TOF into tof_out */
     double drc_eps;        /* pck_drc only: relative k perturbation */
+    const double* t_out;   /* pck_solve: n_out ascending sample times in [t0, t_end] (device), or NULL */
+    int64_t n_out;         /*   the state at each is written to pck_outputs.traj (dense output) */
 } pck_solve_params;
 
 /* Outputs of pck_solve (device pointers; any may be NULL). */
@@ -151,6 +153,9 @@ typedef struct {
     int32_t* nsteps;           /* [n] accepted + rejected steps */
     double* kf; double* kr;    /* [NRXN][ld_k] optional rate-constant dump */
     int64_t ld_k;
+    double* traj; int64_t ld_traj;   /* [n_out][NS][ld_traj] states at pck_solve_params.t_out
+                                      * (System.solve_odes' solution, old_system.py:350-376);
+                                      * needs the hipRTC-specialised kernels (PCK_JIT != 0) */
 } pck_outputs;
 
 /* per-condition status codes */

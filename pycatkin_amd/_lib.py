@@ -49,12 +49,13 @@ class Conditions(C.Structure):
 class SolveParams(C.Structure):
     _fields_ = [('t0', C.c_double), ('t_end', C.c_double), ('rtol', C.c_double), ('atol', C.c_double),
                 ('max_steps', C.c_int32), ('newton', C.c_int32), ('newton_iters', C.c_int32),
-                ('want_activity', C.c_int32), ('drc_eps', C.c_double)]
+                ('want_activity', C.c_int32), ('drc_eps', C.c_double), ('t_out', C.c_void_p), ('n_out', C.c_int64)]
 
 
 class Outputs(C.Structure):
     _fields_ = [('y', C.c_void_p), ('ld_y', C.c_int64), ('tof', C.c_void_p), ('status', C.c_void_p),
-                ('nsteps', C.c_void_p), ('kf', C.c_void_p), ('kr', C.c_void_p), ('ld_k', C.c_int64)]
+                ('nsteps', C.c_void_p), ('kf', C.c_void_p), ('kr', C.c_void_p), ('ld_k', C.c_int64),
+                ('traj', C.c_void_p), ('ld_traj', C.c_int64)]
 
 
 _lib = None

@@ -391,9 +391,11 @@ class System:
 
     def solve_batch(self, T=None, p=None, desc=None, y0=None, fix=None, inflow=None, tof_terms=(),
                     steady=False, activity=False, t_end=None, t0=None, rtol=None, atol=None, max_steps=200000,
-                    newton_iters=30, to_numpy=True):
+                    newton_iters=30, to_numpy=True, t_out=None):
         """Transient solve to t_end (solve_odes), optionally polished to the
-        steady state (find_steady), with TOF or activity per condition."""
+        steady state (find_steady), with TOF or activity per condition; with
+        t_out, also the dynamic state at those times ('traj' [n_out, NS, n],
+        Rodas4 dense output)."""
         plan = self.plan(tuple(tof_terms), None)
         net = self.device(tuple(tof_terms), None)
         sizes = [T, p] + (list(desc.values()) if desc else [])
@@ -406,7 +408,8 @@ class System:
                         t0=times[0] if t0 is None else t0, t_end=times[-1] if t_end is None else t_end,
                         rtol=self.params['rtol'] if rtol is None else rtol,
                         atol=self.params['atol'] if atol is None else atol,
-                        max_steps=max_steps, newton=steady, newton_iters=newton_iters, activity=activity)
+                        max_steps=max_steps, newton=steady, newton_iters=newton_iters, activity=activity,
+                        t_out=t_out)
         if to_numpy:
             return {k: v.cpu().numpy() for k, v in out.items()}
         return out
@@ -447,14 +450,79 @@ class System:
             y[pos[s]] = ydyn[i]
         return y
 
+    def output_times(self):
+        """old_system.py:363-368: [0] + nsteps log-spaced times from times[0]
+        (1e-8 if 0) to times[-1] -- the reference's `ode` path output grid.
+        The `solve_ivp` path stores every BDF step instead (old_system.py:350-358),
+        which no other integrator reproduces; it gets the same grid here."""
+        t0, t1 = float(self.params['times'][0]), float(self.params['times'][-1])
+        n = int(self.params['nsteps'])
+        return np.concatenate((np.zeros(1), np.logspace(np.log10(t0 if t0 else 1.0e-8), np.log10(t1), num=n,
+                                                         endpoint=True)))
+
     def solve_odes(self):
-        """old_system.py:315-383: integrate params['times'][0] -> [-1] (final state kept)."""
+        """old_system.py:315-383: integrate params['times'][0] -> [-1]; self.times /
+        self.solution hold the state at output_times() (device dense output)."""
         plan = self.plan()
-        r = self.solve_batch(T=[self.params['temperature']])
+        times = self.output_times()
+        inside = times[times >= float(self.params['times'][0])]
+        r = self.solve_batch(T=[self.params['temperature']], t_out=inside)
         self._check(r['status'][0], 'solve_odes')
-        self.times = np.array([self.params['times'][0], self.params['times'][-1]])
-        self.solution = np.stack([self._full(plan, plan.y0_default), self._full(plan, r['y'][:, 0])])
+        traj = r['traj'][:, :, 0]
+        sol = np.empty((times.size, len(plan.species)))
+        sol[:times.size - inside.size] = self._full(plan, plan.y0_default)
+        for k in range(inside.size):
+            sol[times.size - inside.size + k] = self._full(plan, traj[k])
+        self.times = times
+        self.solution = sol
         return self.solution
+
+    def write_results(self, path=''):
+        """old_system.py:531-568: rates_/coverages_/pressures_<T>K_<p>bar.csv over
+        self.times (forward and reverse rate of every reaction at each sample
+        from one device launch of pck_reaction_rates)."""
+        import os
+        import pandas as pd
+        if path != '' and not os.path.isdir(path):
+            os.makedirs(path, exist_ok=True)
+        plan = self.plan()
+        T = self.params['temperature']
+        p = self.params['pressure']
+        tag = ('%1.1f' % T) + 'K_' + ('%1.1f' % (p / bartoPa)) + 'bar.csv'
+        names = list(plan.species)
+        st = self.states
+        ads = [i for i, s in enumerate(names) if st[s].state_type in ('adsorbate', 'surface') and s in plan.dyn + plan.fix]
+        gas = [i for i, s in enumerate(names) if st[s].state_type == 'gas' and s in plan.dyn + plan.fix]
+        rates = self._rates_at(plan, self.solution)
+        rheader = ['Time (s)'] + [x for r in self.reactions.values() for x in (r.name + '_fwd', r.name + '_rev')]
+        times = self.times.reshape(-1, 1)
+        pd.DataFrame(np.concatenate((times, rates), axis=1), columns=rheader).to_csv(path + 'rates_' + tag,
+                                                                                     index=False)
+        pd.DataFrame(np.concatenate((times, self.solution[:, ads]), axis=1),
+                     columns=['Time (s)'] + [names[i] for i in ads]).to_csv(path + 'coverages_' + tag, index=False)
+        pd.DataFrame(np.concatenate((times, self.solution[:, gas]), axis=1),
+                     columns=['Time (s)'] + [names[i] for i in gas]).to_csv(path + 'pressures_' + tag, index=False)
+
+    def _rates_at(self, plan, full_states):
+        """[n_samples, 2 * n_reactions] (fwd, rev interleaved, reference order) at
+        full state vectors (classic units), one pck_reaction_rates launch."""
+        net = self.device()
+        m = full_states.shape[0]
+        pos = {s: i for i, s in enumerate(plan.species)}
+        yd = np.stack([full_states[:, pos[s]] for s in plan.dyn]) if plan.dyn else np.zeros((0, m))
+        fx = (np.stack([full_states[:, pos[s]] for s in plan.fix]) * plan.fix_conc_factor[:, None]
+              if plan.fix else None)
+        T = np.full(m, float(self.params['temperature']))
+        Tt, p, d, _, _, _ = self._inputs(net, plan, m, T, None, None, None, None, None)
+        kf, kr = net.rate_constants(m, Tt, p, d)
+        rf, rr = net.reaction_rates(m, Tt, p, yd, kf, kr, d, fx)
+        rf, rr = rf.cpu().numpy(), rr.cpu().numpy()
+        out = np.zeros((m, 2 * len(plan.all_reactions)))
+        for j, name in enumerate(plan.all_reactions):
+            if name in plan.reactions:
+                a = plan.reactions.index(name)
+                out[:, 2 * j], out[:, 2 * j + 1] = rf[a], rr[a]
+        return out
 
     def find_steady(self, *args, **kw):
         """old_system.py:385-468 find_steady(store_steady, plot_comparison, path) for

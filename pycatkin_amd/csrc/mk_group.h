@@ -363,12 +363,17 @@ __device__ __forceinline__ double grp_solve(const Grp<NSP>& x, const LU<NSP>& F,
 // RODAS4 on the group (same scheme, controller, projection and positivity
 // rule as mk_solver.h: integrate)
 // ---------------------------------------------------------------------------
-template <int NSP, int G, int P>
+template <int NSP, int G, int P, bool TRAJ = false>
 __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& gv, const Grp<NSP>& x, double& y,
                                              double t0, double t_end, double rtol, double atol, int max_steps,
-                                             int& nsteps, bool crows) {
+                                             int& nsteps, bool crows, const TrajOut& to) {
     using namespace rodas4;
     const int NS = x.NS;
+    int ko = 0;
+    if constexpr (TRAJ) {                       // samples at or before t0: the initial state
+        for (; ko < to.n && to.t[ko] <= t0; ++ko)
+            if (x.row) to.y[((int64_t)ko * NS + x.gl) * to.ld + to.c] = y;
+    }
     const double invNS = 1.0 / NS;
     nsteps = 0;
     const double span = t_end - t0;
@@ -451,6 +456,12 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
         double u = y + a51 * k1 + a52 * k2 + a53 * k3 + a54 * k4;
         fu = grp_rhs<NSP, G>(gv, x, u);
         const double k5 = grp_solve<NSP, G>(x, F, keep * (fu + ih * (C51 * k1 + C52 * k2 + C53 * k3 + C54 * k4)));
+        double d2 = 0.0, d3 = 0.0;                 // dense output (mk_solver.h: rodas4_dense)
+        if constexpr (TRAJ) {
+            using namespace rodas4_dense;
+            d2 = D21 * k1 + D22 * k2 + D23 * k3 + D24 * k4 + D25 * k5;
+            d3 = D31 * k1 + D32 * k2 + D33 * k3 + D34 * k4 + D35 * k5;
+        }
         u += k5;
         fu = grp_rhs<NSP, G>(gv, x, u);
         const double k6 = grp_solve<NSP, G>(x, F, keep * (fu + ih * (C61 * k1 + C62 * k2 + C63 * k3 + C64 * k4 +
@@ -470,6 +481,7 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
         const double fac = step_factor(q);
         trace(q, 1.0);
         if (q <= 1.0 && pf >= 1.0) {
+            const double t_old = t, y_old = y;
             t = last ? t_end : t + h;
             y = x.row ? fmax(u, 0.0) : 0.0;        // tolerance-level negatives (>= -atol) to 0
 #pragma unroll
@@ -480,6 +492,14 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
                         const double fct = cons0[l] * rcp(sm);
                         if (ci[l] != 0.0) y *= fct;
                     }
+                }
+            }
+            if constexpr (TRAJ) {
+                for (; ko < to.n && to.t[ko] <= t; ++ko) {
+                    const double sv = fmin((to.t[ko] - t_old) / h, 1.0), s1 = 1.0 - sv;
+                    if (x.row)
+                        to.y[((int64_t)ko * NS + x.gl) * to.ld + to.c] =
+                            y_old * s1 + sv * (y + s1 * (d2 * sv + d3 * s1));
                 }
             }
             F0 = grp_rhs<NSP, G>(gv, x, y);
@@ -642,7 +662,7 @@ struct GrpArgs {
     int32_t* nsbuf;     // DRC mode: [M][n] integrator steps per perturbation
 };
 
-template <int NSP, int G, int P>
+template <int NSP, int G, int P, bool TRAJ = false>
 __global__ void __launch_bounds__(64) k_solve_grp(NetView nv, GrpView gv, CondView cv, const double* kf,
                                                   const double* kr, int64_t ld_k, SolveArgs a, GrpArgs ga) {
     extern __shared__ double lds[];
@@ -660,7 +680,9 @@ __global__ void __launch_bounds__(64) k_solve_grp(NetView nv, GrpView gv, CondVi
                       lds + (size_t)grp * grp_lds_doubles(nv.NRXN, NSP, nv.NDYN, gv.ND, ga.QB), ga.QB, x, T);
     double y = x.row ? cv.y0[x.gl * cv.ld_y0 + c * cv.s_y0] : 0.0;
     int ns = 0;
-    int st = grp_integrate<NSP, G, P>(nv, gv, x, y, a.t0, a.t_end, a.rtol, a.atol, a.max_steps, ns, a.cons_rows != 0);
+    TrajOut to{a.t_out, a.n_out, a.traj, a.ld_traj, c};
+    int st = grp_integrate<NSP, G, P, TRAJ>(nv, gv, x, y, a.t0, a.t_end, a.rtol, a.atol, a.max_steps, ns,
+                                            a.cons_rows != 0, to);
     if (st == PCK_ST_OK && a.newton) st = grp_newton<NSP, G, P>(nv, gv, x, y, a.newton_iters);
     const double tof = grp_tof<NSP, G>(nv, gv, x, y);
     const bool fin = gmin<G>((!x.row || isfinite(y)) ? 1.0 : 0.0) > 0.0 && isfinite(tof);

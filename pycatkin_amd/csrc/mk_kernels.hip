@@ -328,7 +328,7 @@ extern "C" int pck_network_create(const int32_t* ip, int64_t n_ip, const double*
         if (h == T::DIGEST && nv.NDYN == T::NS && nv.NRXN == T::R && nv.NCONS == T::NCONS) net->spec = id;
         PCK_COMPILED_NETWORKS(PCK_MATCH)
 #undef PCK_MATCH
-        if (!net->spec && nv.NDYN >= 1 && nv.NDYN <= PCK_MAX_DYN_LANE)
+        if (nv.NDYN >= 1 && nv.NDYN <= PCK_MAX_DYN_LANE)        // hipRTC plan (also for trajectory solves)
             net->jit_src = jit_source(nv.NDYN, nv.NRXN, nv.NCONS, ip + oef, ip + oer, dp + doff[PCK_D_STOICH],
                                       dp + doff[PCK_D_DYN], dp + doff[PCK_D_CONS], ip + ocp);
     }
@@ -602,6 +602,14 @@ static int launch_solve(pck_network* net, const pck_conditions* cond, const pck_
     a.t0 = prm->t0; a.t_end = prm->t_end; a.rtol = prm->rtol; a.atol = prm->atol; a.eps = prm->drc_eps;
     a.max_steps = prm->max_steps; a.newton = prm->newton; a.newton_iters = prm->newton_iters;
     a.want_activity = prm->want_activity;
+    const bool traj = (prm->n_out > 0 && a.traj != nullptr);
+    if (traj) {
+        if (!prm->t_out) return fail(PCK_E_ARG, "n_out > 0 without t_out%s", "");
+        if (drc_groups || a.G != 1) return fail(PCK_E_ARG, "trajectory output is for pck_solve only%s", "");
+        if (!jit_enabled()) return fail(PCK_E_ARG, "trajectory output needs the hipRTC kernels (PCK_JIT=0 is set)%s", "");
+        a.t_out = prm->t_out;
+        a.n_out = (int)prm->n_out;
+    }
     {
         // conservation rows in the stage systems (mk_solver.h: cons_rows) are
         // off by default: measured on examples/DMTM at 400 K they cost 1.5x
@@ -634,7 +642,8 @@ static int launch_solve(pck_network* net, const pck_conditions* cond, const pck_
         dim3 g((unsigned)((groups + per - 1) / per));
         hipFunction_t f = nullptr;
         int P = grp_p(NS);
-        if (net->plan_mode != PCK_PLAN_RUNTIME && jit_enabled()) f = jit_group_kernel(NS, G, P);
+        if ((net->plan_mode != PCK_PLAN_RUNTIME || traj) && jit_enabled()) f = jit_group_kernel(NS, G, P, traj);
+        if (traj && !f) return fail(PCK_E_HIP, "hipRTC compile of the trajectory kernel failed%s", "");
         size_t shm;
         if (f) {
             rc = grp_shape(net, NS, P, &shm, &ga.QB);
@@ -667,7 +676,17 @@ static int launch_solve(pck_network* net, const pck_conditions* cond, const pck_
     const int64_t lanes = n * a.G;
     const size_t shm = lds_bytes(R, net->nv.NDYN, B);
     dim3 g((unsigned)((lanes + B - 1) / B));
-    if (net->spec && net->plan_mode == PCK_PLAN_AUTO) {
+    if (traj) {
+        hipFunction_t f = net->jit_src.empty() ? nullptr : jit_kernel(net->digest, net->jit_src, true);
+        if (!f) return fail(PCK_E_HIP, "hipRTC compile of the trajectory kernel failed%s", "");
+        NetView nv = net->nv;
+        CondView cv = cview(cond);
+        const double* kfp = kf;
+        const double* krp = kr;
+        int64_t ldk = n;
+        void* args[] = {&nv, &cv, &kfp, &krp, &ldk, &a};
+        HIPCHK(hipModuleLaunchKernel(f, g.x, 1, 1, B, 1, 1, (unsigned)shm, s, args, nullptr));
+    } else if (net->spec && net->plan_mode == PCK_PLAN_AUTO) {
 #define PCK_LAUNCH_CT(id, T)                                                                           \
         if (net->spec == id)                                                                          \
             hipLaunchKernelGGL(k_solve<PlanCT<T>>, g, dim3(B), shm, s, net->nv, cview(cond), kf, kr, n, a);
@@ -708,6 +727,11 @@ extern "C" int pck_solve(const pck_network* net, const pck_conditions* cond, con
     memset(&a, 0, sizeof(a));
     a.y = out->y; a.ld_y = out->ld_y; a.tof = out->tof; a.status = out->status; a.nsteps = out->nsteps;
     a.G = 1;
+    if (prm->n_out > 0 && out->traj) {
+        if (out->ld_traj < cond->n) return fail(PCK_E_ARG, "ld_traj%s too small", "");
+        a.traj = out->traj;
+        a.ld_traj = out->ld_traj;
+    }
     if ((out->kf || out->kr) && cond->n > 0 && (out->ld_k < cond->n || !out->kf || !out->kr))
         return fail(PCK_E_ARG, "kf/kr dump needs both arrays%s", "");
     // the network is not modified; const_cast only for the hipRTC bookkeeping flag

@@ -286,11 +286,42 @@ constexpr double C61 = 8.083246795921522, C62 = -7.981132988064893, C63 = -31.52
                  C64 = 16.31930543123136, C65 = -6.058818238834054;
 }  // namespace rodas4
 
-template <class P, class K>
-__device__ int integrate(const P& p, const Lane<P::NS>& L, const K& k, double (&y)[P::NS], double t0,
-                         double t_end, double rtol, double atol, int max_steps, int& nsteps, bool crows) {
+// Dense output of RODAS4 (Hairer & Wanner's rodas.f, METH=1): over an
+// accepted step y0 -> y1 of size h,
+//   y(t0 + s h) = (1-s) y0 + s (y1 + (1-s) (s d2 + (1-s) d3)),
+//   d2 = sum_j D2j k_j,  d3 = sum_j D3j k_j  (j = 1..5),
+// third order, the continuous extension the reference's `ode` (lsoda) path
+// samples at its log-spaced output times (old_system.py:359-376).
+namespace rodas4_dense {
+constexpr double D21 = 10.12623508344586, D22 = -7.487995877610167, D23 = -34.80091861555747,
+                 D24 = -7.992771707568823, D25 = 1.025137723295662;
+constexpr double D31 = -0.6762803392801253, D32 = 6.087714651680015, D33 = 16.43084320892478,
+                 D34 = 24.76722511418386, D35 = -6.594389125716872;
+}  // namespace rodas4_dense
+
+// Trajectory samples of one condition: state at the shared times t[0..n)
+// into y[(k*NS + i)*ld + c]
+struct TrajOut {
+    const double* t;
+    int n;
+    double* y;
+    int64_t ld;
+    int64_t c;
+};
+
+template <bool TRAJ, class P, class K>
+__device__ __forceinline__ int integrate(const P& p, const Lane<P::NS>& L, const K& k, double (&y)[P::NS], double t0,
+                         double t_end, double rtol, double atol, int max_steps, int& nsteps, bool crows,
+                         const TrajOut& to) {
     using namespace rodas4;
     constexpr int NS = P::NS;
+    int ko = 0;
+    if constexpr (TRAJ) {
+        for (; ko < to.n && to.t[ko] <= t0; ++ko) {
+#pragma unroll
+            for (int i = 0; i < NS; ++i) to.y[((int64_t)ko * NS + i) * to.ld + to.c] = y[i];
+        }
+    }
     nsteps = 0;
     const double span = t_end - t0;
     if (!(span > 0.0)) return PCK_ST_OK;
@@ -390,6 +421,15 @@ __device__ int integrate(const P& p, const Lane<P::NS>& L, const K& k, double (&
         for (int i = 0; i < NS; ++i) k5[i] = fu[i] + ih * (C51 * k1[i] + C52 * k2[i] + C53 * k3[i] + C54 * k4[i]);
         if (crows) cons_zero(p, k5);
         lu_solve<NS>(W, piv, sw, k5);
+        double d2[TRAJ ? NS : 1], d3[TRAJ ? NS : 1];
+        if constexpr (TRAJ) {
+            using namespace rodas4_dense;
+#pragma unroll
+            for (int i = 0; i < NS; ++i) {
+                d2[i] = D21 * k1[i] + D22 * k2[i] + D23 * k3[i] + D24 * k4[i] + D25 * k5[i];
+                d3[i] = D31 * k1[i] + D32 * k2[i] + D33 * k3[i] + D34 * k4[i] + D35 * k5[i];
+            }
+        }
 #pragma unroll
         for (int i = 0; i < NS; ++i) u[i] += k5[i];
         rhs(p, L, k, u, fu);
@@ -425,7 +465,13 @@ __device__ int integrate(const P& p, const Lane<P::NS>& L, const K& k, double (&
         }
         const double fac = step_factor(q);
         if (q <= 1.0 && pf >= 1.0) {
+            const double t_old = t;
             t = last ? t_end : t + h;
+            double y_old[TRAJ ? NS : 1];
+            if constexpr (TRAJ) {
+#pragma unroll
+                for (int i = 0; i < NS; ++i) y_old[i] = y[i];
+            }
 #pragma unroll
             for (int i = 0; i < NS; ++i) y[i] = fmax(u[i], 0.0);     // tolerance-level negatives (>= -atol) to 0
             // Rosenbrock stages keep linear invariants only up to the rounding of
@@ -444,6 +490,16 @@ __device__ int integrate(const P& p, const Lane<P::NS>& L, const K& k, double (&
 #pragma unroll
                     for (int i = 0; i < NS; ++i)
                         if (p.C(l, i) != 0.0) y[i] *= fct;
+                }
+            }
+            if constexpr (TRAJ) {
+                // samples inside (t_old, t]: the dense output of this step
+                for (; ko < to.n && to.t[ko] <= t; ++ko) {
+                    const double sv = fmin((to.t[ko] - t_old) / h, 1.0), s1 = 1.0 - sv;
+#pragma unroll
+                    for (int i = 0; i < NS; ++i)
+                        to.y[((int64_t)ko * NS + i) * to.ld + to.c] =
+                            y_old[i] * s1 + sv * (y[i] + s1 * (d2[i] * sv + d3[i] * s1));
                 }
             }
             rhs(p, L, k, y, F0);
@@ -470,7 +526,7 @@ __device__ int integrate(const P& p, const Lane<P::NS>& L, const K& k, double (&
 // convergent (a site-starved surface approached algebraically) or lands on a
 // negative component is not regular -> PCK_ST_NEWTON, transient state kept.
 template <class P, class K>
-__device__ int newton(const P& p, const Lane<P::NS>& L, const K& k, double (&y)[P::NS], int iters) {
+__device__ __forceinline__ int newton(const P& p, const Lane<P::NS>& L, const K& k, double (&y)[P::NS], int iters) {
     constexpr int NS = P::NS;
     double b[PCK_MAX_CONS];
     for (int l = 0; l < p.ncons(); ++l) {
@@ -634,7 +690,9 @@ struct SolveArgs {
     double* tof; int32_t* status; int32_t* nsteps;
     double* xi; int64_t ld_xi; double* tof0;   // DRC mode
     int G;                                     // lanes per condition (1, or DRC group size)
-    int cons_rows;                             // conservation rows in the stage systems (A/B: PCK_CONS_ROWS=0)
+    int cons_rows;                             // conservation rows in the stage systems (A/B: PCK_CONS_ROWS=1)
+    const double* t_out; int n_out;            // trajectory sample times (k_solve<P, true>)
+    double* traj; int64_t ld_traj;             // [n_out][NS][ld_traj]
 };
 
 template <class P>
@@ -657,7 +715,7 @@ struct KFor<PlanCT<Net>> {
 #define PCK_SOLVE_WAVES 1
 #endif
 
-template <class P>
+template <class P, bool TRAJ = false>
 __global__ void __launch_bounds__(PCK_SOLVE_BLOCK) __attribute__((amdgpu_waves_per_eu(PCK_SOLVE_WAVES))) k_solve(NetView nv, CondView cv, const double* kf, const double* kr,
                                                int64_t ld_k, SolveArgs a) {
     constexpr int NS = P::NS;
@@ -692,7 +750,8 @@ __global__ void __launch_bounds__(PCK_SOLVE_BLOCK) __attribute__((amdgpu_waves_p
         double y[NS];
 #pragma unroll
         for (int i = 0; i < NS; ++i) y[i] = cv.y0[i * cv.ld_y0 + c * cv.s_y0];
-        st = integrate(p, L, k, y, a.t0, a.t_end, a.rtol, a.atol, a.max_steps, ns, a.cons_rows != 0);
+        TrajOut to{a.t_out, a.n_out, a.traj, a.ld_traj, c};
+        st = integrate<TRAJ>(p, L, k, y, a.t0, a.t_end, a.rtol, a.atol, a.max_steps, ns, a.cons_rows != 0, to);
         if (st == PCK_ST_OK && a.newton) st = newton(p, L, k, y, a.newton_iters);
         tof = lane_tof(p, nv, k, y);
         bool fin = isfinite(tof);

@@ -177,11 +177,18 @@ class DeviceNetwork:
         p.want_activity, p.drc_eps = int(bool(activity)), float(drc_eps)
         return p
 
-    def solve(self, n, T, p, y0, desc=None, fixc=None, inflow=None, want_k=False, out=None, **kw):
-        """pck_solve: returns dict(y [NS,n], tof [n] (or activity), status, nsteps)."""
+    def solve(self, n, T, p, y0, desc=None, fixc=None, inflow=None, want_k=False, out=None, t_out=None, **kw):
+        """pck_solve: returns dict(y [NS,n], tof [n] (or activity), status, nsteps)
+        and, with t_out (ascending sample times), traj [n_out, NS, n]."""
         torch = self.torch
         c, keep = self.conditions(n, T, p, desc, fixc, y0, inflow)
         prm = self.params(**kw)
+        tt = None
+        if t_out is not None:
+            tt = torch.as_tensor(np.asarray(t_out, float).ravel(), dtype=torch.float64, device='cuda').contiguous()
+            if tt.numel() and bool((tt[1:] < tt[:-1]).any()):
+                raise ValueError('t_out must be ascending')
+            prm.t_out, prm.n_out = _ptr(tt).value, int(tt.numel())
         if out is None:
             out = dict(y=torch.empty((self.NDYN, n), dtype=torch.float64, device='cuda'),
                        tof=torch.empty(n, dtype=torch.float64, device='cuda'),
@@ -195,6 +202,9 @@ class DeviceNetwork:
         o.tof, o.status, o.nsteps = _ptr(out['tof']), _ptr(out['status']), _ptr(out['nsteps'])
         if 'kf' in out:
             o.kf, o.kr, o.ld_k = _ptr(out['kf']), _ptr(out['kr']), n
+        if tt is not None and tt.numel():
+            out['traj'] = torch.empty((tt.numel(), self.NDYN, n), dtype=torch.float64, device='cuda')
+            o.traj, o.ld_traj = _ptr(out['traj']), n
         L.check(self.lib.pck_solve(self.h, C.byref(c), C.byref(prm), C.byref(o), _stream(torch)))
         return out
 

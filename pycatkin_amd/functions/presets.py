@@ -15,8 +15,12 @@ from ..constants.physical_constants import bartoPa
 
 
 def run(sim_system, steady_state_solve=False, plot_results=False, save_results=False, fig_path=None, csv_path=''):
-    """presets.py:16-28"""
+    """presets.py:16-28 (plotting is out of scope: plot_results raises)."""
+    if plot_results:
+        raise NotImplementedError('plotting (System.plot_transient) is not part of pycatkin_amd')
     sim_system.solve_odes()
+    if save_results:
+        sim_system.write_results(path=csv_path)
     if steady_state_solve:
         sim_system._find_steady_classic(store_steady=True)
 

@@ -452,7 +452,9 @@ def test_ch4_steady_state_solver(P, inputs):
         xp, yp = s._to_plan(s.plan(), x[:, None])[:, 0], s._to_plan(s.plan(), solver2._norm(yT)[:, None])[:, 0]
         np.testing.assert_allclose(C @ xp, C @ yp, rtol=1e-10, atol=1e-14)
     r2 = solver2.solve_root()
-    assert r2.success == solver2.test_convergence(r2.x)
+    # success only when the root itself passes the reference's checks
+    # (solver.py:279-291); otherwise the best-scored candidate comes back
+    assert (not r2.success) or solver2.test_convergence(r2.x)
     Y, ok = solver.solve_ode_batch(T=[473.0, 523.0, 573.0])
     assert ok[1] == res.success
     np.testing.assert_allclose(Y[:, 1], res.x, rtol=1e-12, atol=1e-300)

@@ -432,3 +432,54 @@ def test_degenerate_roots_vs_least_squares(P, inputs):
         aT = m.activity(m.tof(yT, ['CO_ox']))
         assert abs(act[0, 0] - aT) <= 1e-4 * abs(aT), (eco, eo, act[0, 0], aT)
     assert n4 >= 3, n4
+
+
+@pytest.mark.parametrize('which', ['cstr', 'dmtm'])
+def test_trajectory_dense_output_vs_oracle(P, inputs, which, tmp_path):
+    """System.solve_odes() keeps the whole trajectory (old_system.py:350-376):
+    the state at the reference's log-spaced output times from the device
+    Rodas4 dense output (one-lane path: the Pd111 CSTR; lane-group path: DMTM) vs
+    scipy BDF sampled at the same times (t_eval).  Both at rtol 1e-10 /
+    atol 1e-14; agreement 1e-5 relative (1e-12 absolute floor).  Then
+    write_results / run(save_results=True) write the reference's three CSVs."""
+    from pycatkin_amd.functions.presets import run
+    if which == 'cstr':
+        s = P.read_from_input_file(os.path.join(inputs, 'COOxReactor', 'input_Pd111.json'))
+        spec = O.load_spec(os.path.join(inputs, 'COOxReactor', 'input_Pd111.json'))
+    else:
+        s = P.read_from_input_file(os.path.join(inputs, 'DMTM', 'input.json'))
+        spec = O.load_spec(os.path.join(inputs, 'DMTM', 'input.json'))
+    s.params.update(rtol=1e-10, atol=1e-14, nsteps=60)
+    sol = s.solve_odes()
+    times = s.times
+    assert times.size == 61 and times[0] == 0.0 and sol.shape[0] == 61
+    m = O.ClassicModel(spec)
+    from scipy.integrate import solve_ivp
+    ref = solve_ivp(lambda t, y: m.rhs(y), (times[0], times[-1]), m.y0, method='BDF', jac=lambda t, y: m.jac(y),
+                    rtol=1e-10, atol=1e-14, t_eval=times)
+    assert ref.status == 0
+    plan = s.plan()
+    dyn = [plan.species.index(n) for n in plan.dyn]
+    odyn = [m.idx[n] for n in plan.dyn]
+    got, exp = sol[:, dyn], ref.y[odyn].T
+    assert np.all(np.abs(got - exp) <= 1e-5 * np.abs(exp) + 1e-12), np.abs(got - exp).max()
+    s.write_results(path=str(tmp_path) + '/')
+    import glob
+    import pandas as pd
+    files = sorted(os.path.basename(f).split('_')[0] for f in glob.glob(str(tmp_path) + '/*.csv'))
+    assert files == ['coverages', 'pressures', 'rates']
+    cov = pd.read_csv(glob.glob(str(tmp_path) + '/coverages_*.csv')[0])
+    assert list(cov.columns)[0] == 'Time (s)' and len(cov) == 61
+    np.testing.assert_allclose(cov['Time (s)'].values, times)
+    rates = pd.read_csv(glob.glob(str(tmp_path) + '/rates_*.csv')[0])
+    assert len(rates.columns) == 1 + 2 * len(s.reactions)
+    # rates at the last sample = the oracle's reaction rates at that state
+    last = sol[-1]
+    full = m.y0.copy()
+    for n in plan.species:
+        full[m.idx[n]] = last[plan.species.index(n)]
+    rr = m.rates(full)
+    np.testing.assert_allclose(rates.values[-1, 1:].reshape(-1, 2), rr, rtol=1e-9, atol=1e-300)
+    out = tmp_path / 'run'
+    run(s, save_results=True, csv_path=str(out) + '/')
+    assert len(glob.glob(str(out) + '/*.csv')) == 3

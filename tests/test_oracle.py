@@ -166,3 +166,13 @@ def test_outcar_reader_matches_oracle(inputs):
     for d in ('CO', 'O2', 'CO2'):
         I = read_outcar(os.path.join(data, d)).moments_of_inertia()
         assert np.sum(I > 1e-12) == 2
+
+
+def test_output_times_follow_the_reference_ode_grid():
+    """old_system.py:363-368: [0] + nsteps log-spaced times from times[0] (1e-8 when 0)."""
+    import pycatkin_amd as P
+    s = P.System(times=[0.0, 3600.0], nsteps=5)
+    t = s.output_times()
+    np.testing.assert_allclose(t, np.concatenate(([0.0], np.logspace(-8, np.log10(3600.0), 5))))
+    s = P.System(times=[1.0, 1.0e4], nsteps=3)
+    np.testing.assert_allclose(s.output_times(), [0.0, 1.0, 100.0, 1.0e4])
