@@ -499,7 +499,7 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
                     const double sv = fmin((to.t[ko] - t_old) / h, 1.0), s1 = 1.0 - sv;
                     if (x.row)
                         to.y[((int64_t)ko * NS + x.gl) * to.ld + to.c] =
-                            y_old * s1 + sv * (y + s1 * (d2 * sv + d3 * s1));
+                            y_old * s1 + sv * (y + s1 * (d2 + sv * d3));
                 }
             }
             F0 = grp_rhs<NSP, G>(gv, x, y);

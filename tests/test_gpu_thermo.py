@@ -8,9 +8,12 @@ scaling states, restated with ASE's published HarmonicThermo formulas
     ZPE = 1/2 sum eps,   F = E + ZPE + kB T sum ln(1 - exp(-eps / kB T)),
     eps = invcm * nu[cm^-1],  ASE's CODATA-2014 constants.
 
-tests.py asserts ceil-rounded equality at 6 / 3 / 3 decimals (its my_round);
-the same assertions hold here, and the values agree to the 1e-4 eV the two
-constant sets differ by.  The O2 gas free energy (tests.py:105-117 only
+tests.py asserts ceil-rounded equality at 6 / 3 / 3 decimals (its my_round)
+on sCO and sC-H--OH (tests.py:121-122); the same assertions are made on those
+two here.  For every state the values agree to the ~1e-4 eV the two constant
+sets differ by (PyCatKin's h = 6.626176e-34, JtoeV = 6.242e18 vs ASE's
+CODATA 2014: ZPEs differ by 9.5e-5 relative, which moves the ceil-rounded
+third decimal of sCH3's ZPE -- a state tests.py never rounds).  The O2 gas free energy (tests.py:105-117 only
 prints it) is checked against IdealGasThermo's linear-molecule Gibbs energy
 without its electronic-spin term kB T ln(2S+1), which PyCatKin does not
 include (state.py:320-365)."""
@@ -40,6 +43,7 @@ STATES = {   # test/tests.py:46-51, 134-157: (coefficients for [EC, EO, 1], freq
     'sCH2': ([0.494635, 0, 0.232988], [152.0, 257.5, 305.9, 416.3, 434.8, 643.3, 1329.9, 2947.9, 3008.0]),
     'hH': ([0.219820574, 0, -0.785276035], [978.2, 768.0, 764.8]),
 }
+ROUNDED = ('sCO', 'sC-H--OH')   # the states tests.py:121-122 passes to test_energy
 
 
 def my_round(n, n_dec=4):
@@ -74,8 +78,10 @@ def test_scaling_state_energies_vs_harmonic_thermo(ch4, name):
     st.calc_zpe()
     Gfree = st.get_free_energy(T, p)                       # device: kernel 1 energy program
     assert my_round(E_pred, 6) == my_round(Gelec, 6)       # tests.py:100
-    assert my_round(zpe, 3) == my_round(st.Gzpe, 3)        # tests.py:101
-    assert my_round(A_pred, 3) == my_round(Gfree, 3)       # tests.py:102
+    if name in ROUNDED:
+        assert my_round(zpe, 3) == my_round(st.Gzpe, 3)    # tests.py:101
+        assert my_round(A_pred, 3) == my_round(Gfree, 3)   # tests.py:102
+    assert abs(st.Gzpe - zpe) <= 1.5e-4 * zpe, (st.Gzpe, zpe)
     assert abs(Gfree - A_pred) < 2e-4, (Gfree, A_pred)
 
 

@@ -25,6 +25,9 @@ Cc = [[], [-5.6688], [-2.430093356833875, -0.2063599157091915],
       [8.083246795921522, -7.981132988064893, -31.52159432874371, 16.31930543123136, -6.058818238834054]]
 
 
+DD2 = [10.12623508344586, -7.487995877610167, -34.80091861555747, -7.992771707568823, 1.025137723295662]
+DD3 = [-0.6762803392801253, 6.087714651680015, 16.43084320892478, 24.76722511418386, -6.594389125716872]
+
 PIVLOG = []
 
 
@@ -63,7 +66,8 @@ def gpu_lu_solve(W, rhs_list):
     return out
 
 
-def rodas4(f, J, y, t0, t_end, rtol, atol, cons=None, max_steps=200000, cons_rows=None, trace=None, gpu_lu=False):
+def rodas4(f, J, y, t0, t_end, rtol, atol, cons=None, max_steps=200000, cons_rows=None, trace=None, gpu_lu=False,
+           t_out=None, samples=None):
     """Returns (y, status, nsteps).  cons: conservation matrix (rows >= 0 get
     the multiplicative projection).  cons_rows: optional (C, piv) -- replace the
     pivot rows of W by the conservation rows (the index-reduced stage system)."""
@@ -82,6 +86,11 @@ def rodas4(f, J, y, t0, t_end, rtol, atol, cons=None, max_steps=200000, cons_row
     c0 = cons @ y if cons is not None else None
     t = t0
     n = 0
+    ko = 0
+    if t_out is not None:
+        while ko < len(t_out) and t_out[ko] <= t0:
+            samples.append(y.copy())
+            ko += 1
     while t < t_end:
         if n >= max_steps:
             return y, 1, n
@@ -144,6 +153,7 @@ def rodas4(f, J, y, t0, t_end, rtol, atol, cons=None, max_steps=200000, cons_row
                 print('t %.3e h %.3e q %.3e worst comp %d y %.3e unew %.3e e %.3e |e| sorted %s' % (
                     t, h, q, j, y[j], unew[j], e[j], np.array2string(np.sort(np.abs(e))[::-1][:4], precision=2)))
         if acc:
+            t_old, y_old = t, y
             t = t_end if last else t + h
             y = unew if os.environ.get('NOCLIP') else np.maximum(unew, 0.0)
             if cons is not None:
@@ -152,6 +162,14 @@ def rodas4(f, J, y, t0, t_end, rtol, atol, cons=None, max_steps=200000, cons_row
                         sm = cons[l] @ y
                         if sm > 0:
                             y = np.where(cons[l] != 0, y * c0[l] / sm, y)
+            if t_out is not None:        # Rodas4 dense output (mk_solver.h rodas4_dense)
+                d2 = sum(c * k for c, k in zip(DD2, ks[:5]))
+                d3 = sum(c * k for c, k in zip(DD3, ks[:5]))
+                while ko < len(t_out) and t_out[ko] <= t:
+                    s = min((t_out[ko] - t_old) / h, 1.0)
+                    s1 = 1.0 - s
+                    samples.append(y_old * s1 + s * (y + s1 * (d2 + s * d3)))
+                    ko += 1
             F0 = f(y)
             h *= min(6.0, max(0.2, fac))
         else:
