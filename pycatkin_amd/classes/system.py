@@ -415,14 +415,17 @@ class System:
         return out
 
     def drc_batch(self, tof_terms, T=None, p=None, desc=None, eps=1.0e-3, steady=False, t_end=None, rtol=None,
-                  atol=None, max_steps=200000):
+                  atol=None, max_steps=200000, y0=None, fix=None, inflow=None):
         """Degree of rate control of every reaction (old_system.py:490-515) for a batch.
 
         Returns {reaction name: xi [n]} (ghost reactions: 0) plus 'tof0' and 'status'."""
         plan = self.plan(tuple(tof_terms), None)
         net = self.device(tuple(tof_terms), None)
         n = self._n(T, p, *(desc.values() if desc else []))
-        T, p, d, fx, y0, inflow = self._inputs(net, plan, n, T, p, desc, None, None, None)
+        for a in (y0, fix, inflow):
+            if a is not None and np.ndim(a) == 2:
+                n = max(n, np.shape(a)[1])
+        T, p, d, fx, y0, inflow = self._inputs(net, plan, n, T, p, desc, y0, fix, inflow)
         times = self.params['times'] or [0.0, 1.0e4]
         r = net.drc(n, T, p, y0, d, fx, inflow, t0=times[0], t_end=times[-1] if t_end is None else t_end,
                     rtol=self.params['rtol'] if rtol is None else rtol,

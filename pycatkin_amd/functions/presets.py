@@ -85,9 +85,47 @@ def run_temperatures(sim_system, temperatures, steady_state_solve=False, tof_ter
 def run_parameters(sim_system, parameters, params_name, steady_state_solve=False, tof_terms=None, eps=5.0e-2,
                    plot_results=False, save_results=False, plot_transient=False, save_transient=False,
                    fig_path=None, csv_path=''):
-    """presets.py:170-305 as one batch.  params_name: 'temperature', 'pressure',
-    'start_state_<gas>' or 'inflow_state_<gas>'."""
+    """presets.py:170-305.  'temperature', 'pressure', 'start_state_<gas>' and
+    'inflow_state_<gas>' vary per condition inside one batch; any other
+    `params` key (presets.py:187-188: rtol, atol, times, ...) is set value by
+    value, one launch each.  As in the reference, sim_system.params keeps the
+    last value afterwards."""
     vals = np.asarray(parameters, float).ravel()
+    if plot_results or plot_transient:
+        raise NotImplementedError('plotting is out of scope (DESIGN.md); use save_results')
+    batched = (params_name in ('temperature', 'pressure') or params_name.startswith('start_state_')
+               or params_name.startswith('inflow_state_'))
+    if batched:
+        final, rates, drcs = _run_batch(sim_system, params_name, vals, steady_state_solve, tof_terms, eps)
+    else:
+        parts = [_run_batch(sim_system, params_name, vals[k:k + 1], steady_state_solve, tof_terms, eps,
+                            set_param=True) for k in range(vals.size)]
+        final = np.concatenate([q[0] for q in parts], axis=0)
+        rates = np.concatenate([q[1] for q in parts], axis=0)
+        drcs = {}
+        for q in parts:
+            drcs.update(q[2])
+    _keep_last(sim_system, params_name, vals[-1])
+    if save_results:
+        _save(sim_system, sim_system.plan(), params_name, params_name, vals, final, rates, drcs, tof_terms, csv_path)
+    return final, rates, drcs
+
+
+def _keep_last(sim_system, params_name, v):
+    """the reference's loop leaves its last value in sim_system.params (presets.py:181-188)"""
+    if params_name.startswith('start_state_'):
+        sim_system.params['start_state'][params_name.split('start_state_')[1]] = v
+    elif params_name.startswith('inflow_state_'):
+        sim_system.params['inflow_state'][params_name.split('inflow_state_')[1]] = v
+    else:
+        sim_system.params[params_name] = v
+    sim_system._plans.clear()
+
+
+def _run_batch(sim_system, params_name, vals, steady_state_solve, tof_terms, eps, set_param=False):
+    if set_param:
+        sim_system.params[params_name] = float(vals[0])
+        sim_system._plans.clear()
     plan = sim_system.plan()
     kw = {}
     if params_name == 'temperature':
@@ -109,8 +147,6 @@ def run_parameters(sim_system, parameters, params_name, steady_state_solve=False
         inflow = np.tile(plan.inflow_default[:, None], (1, vals.size))
         inflow[plan.dyn.index(s)] = vals
         kw['inflow'] = inflow
-    else:
-        raise KeyError(params_name)
     n = vals.size
     if 'T' not in kw:
         kw['T'] = np.full(n, float(sim_system.params['temperature']))
@@ -122,11 +158,9 @@ def run_parameters(sim_system, parameters, params_name, steady_state_solve=False
     rates = _net_rates(sim_system, plan, final, kw['T'], kw.get('p'))
     drcs = {}
     if tof_terms is not None:
-        d = sim_system.drc_batch(tof_terms, T=kw['T'], p=kw.get('p'), eps=eps)
+        d = sim_system.drc_batch(tof_terms, eps=eps, **kw)
         for k, v in enumerate(vals):
             drcs[v] = {name: float(d[name][k]) for name in sim_system.reactions}
-    if save_results:
-        _save(sim_system, plan, params_name, params_name, vals, final, rates, drcs, tof_terms, csv_path)
     return final, rates, drcs
 
 

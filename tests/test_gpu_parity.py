@@ -483,3 +483,61 @@ def test_trajectory_dense_output_vs_oracle(P, inputs, which, tmp_path):
     out = tmp_path / 'run'
     run(s, save_results=True, csv_path=str(out) + '/')
     assert len(glob.glob(str(out) + '/*.csv')) == 3
+
+
+def test_run_parameters_generic_key_and_start_state(P, inputs):
+    """run_parameters over a params key outside the batched four
+    (presets.py:187-188 sets any key): one launch per value, each equal to a
+    solve with that setting, and the last value left in params as the
+    reference's loop leaves it.  Then a start_state sweep with tof_terms: the
+    DRC of each condition starts from that condition's own start state."""
+    from pycatkin_amd.functions.presets import run_parameters
+    f = os.path.join(inputs, 'COOxReactor', 'input_Pd111.json')
+    s = P.read_from_input_file(f)
+    s.params['temperature'] = 523.0
+    atols = [1e-10, 1e-14]
+    final, rates, _ = run_parameters(s, atols, 'atol')
+    assert s.params['atol'] == 1e-14
+    plan = s.plan()
+    for k, a in enumerate(atols):
+        r = s.solve_batch(T=[523.0], atol=a)
+        got = np.array([final[k, plan.species.index(n)] for n in plan.dyn])
+        np.testing.assert_array_equal(got, r['y'][:, 0])
+    # start state of a gas species: per-condition y0 in the solve and in the DRC
+    s2 = P.read_from_input_file(f)
+    s2.params['temperature'] = 573.0
+    co = [0.0, 0.01, 0.03]
+    final2, _, drcs = run_parameters(s2, co, 'start_state_CO', tof_terms=['CO_ox'], eps=1e-3)
+    assert s2.params['start_state']['CO'] == 0.03
+    plan2 = s2.plan(('CO_ox',))
+    for k, v in enumerate(co):
+        y0 = plan2.y0_default.copy()
+        y0[plan2.dyn.index('CO')] = v
+        d = s2.drc_batch(['CO_ox'], T=[573.0], eps=1e-3, y0=y0[:, None])
+        for name in s2.reactions:
+            assert drcs[co[k]][name] == float(d[name][0]), (v, name)
+
+
+def test_two_streams_share_one_network(P, inputs):
+    """pck_solve keeps no scratch in the network (stream-ordered per-call
+    buffers, include/pycatkin_amd.h): two solves of one network in flight on
+    two HIP streams give exactly the single-stream results."""
+    import torch
+    s = volcano_sys(P, inputs)
+    rng = np.random.default_rng(11)
+    n = 4096
+    d1 = {'ECO': rng.uniform(-2.5, 0.5, n), 'EO': rng.uniform(-2.5, 0.5, n)}
+    d2 = {'ECO': rng.uniform(-2.5, 0.5, n), 'EO': rng.uniform(-2.5, 0.5, n)}
+    kw = dict(T=np.full(n, 600.0), tof_terms=('CO_ox',), steady=True, activity=True)
+    ref1 = s.solve_batch(desc=d1, **kw)
+    ref2 = s.solve_batch(desc=d2, **kw)
+    st1, st2 = torch.cuda.Stream(), torch.cuda.Stream()
+    torch.cuda.synchronize()
+    with torch.cuda.stream(st1):
+        r1 = s.solve_batch(desc=d1, to_numpy=False, **kw)
+    with torch.cuda.stream(st2):
+        r2 = s.solve_batch(desc=d2, to_numpy=False, **kw)
+    torch.cuda.synchronize()
+    for r, ref in ((r1, ref1), (r2, ref2)):
+        for key in ('y', 'tof', 'status'):
+            np.testing.assert_array_equal(r[key].cpu().numpy(), ref[key])
