@@ -43,6 +43,17 @@ namespace pck {
 __device__ long long pck_trace_cond = -1;
 __device__ int pck_trace_pos = 0;
 __device__ double pck_trace_buf[PCK_TRACE_N * PCK_TRACE_W];
+// shader-clock cycles of the traced condition's integrator phases:
+// [jac, lu, solve, rhs, other, steps]
+__device__ double pck_phase[8];
+#define PCK_PH(i, expr)                                              \
+    do {                                                             \
+        const long long t_ph0 = __builtin_readcyclecounter();        \
+        expr;                                                        \
+        if (tr) pck_phase[i] += (double)(__builtin_readcyclecounter() - t_ph0); \
+    } while (0)
+#else
+#define PCK_PH(i, expr) expr
 #endif
 
 #define PCK_GRP_MAX_PART 6   // dynamic participants (species with an exponent) per reaction
@@ -278,6 +289,9 @@ struct LU {
     int step;
 };
 
+#ifndef PCK_GRP_READLANE
+#define PCK_GRP_READLANE 1
+#endif
 template <int NSP, int G>
 __device__ __forceinline__ bool grp_lu(const Grp<NSP>& x, LU<NSP>& F) {
     bool fre = x.row;
@@ -290,7 +304,7 @@ __device__ __forceinline__ bool grp_lu(const Grp<NSP>& x, LU<NSP>& F) {
             int key = fre ? (int)((__float_as_uint(mag) & ~63u) | (uint32_t)x.gl) : -1;
             key = gmaxi<G>(key);
             const int p = key & 63;
-            if constexpr (G == 64) {
+            if constexpr (G == 64 && PCK_GRP_READLANE) {
                 // full wavefront: the pivot row is read straight out of the
                 // pivot lane's registers (v_readlane into SGPRs, used as the
                 // scalar operand of the FMAs) -- no LDS round trip, no copy
@@ -418,7 +432,11 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
         if (t + h >= t_end) { h = t_end - t; last = true; }
         const double ih = rcp(h);
         const double ig = ih * (1.0 / g);
-        grp_jac<NSP, G, P>(nv, gv, x, y, -1.0, ig, F.W);       // W = I/(h g) - J
+#ifdef PCK_TRACE
+        const bool tr = (x.cidx == pck_trace_cond) && x.gl == 0;
+        if (tr) pck_phase[5] += 1.0;
+#endif
+        PCK_PH(0, (grp_jac<NSP, G, P>(nv, gv, x, y, -1.0, ig, F.W)));       // W = I/(h g) - J
         if (cpv >= 0) {                                        // conservation rows (mk_solver.h: cons_rows)
             double m = 0.0;
 #pragma unroll
@@ -427,7 +445,6 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
             for (int q = 0; q < NSP; ++q) F.W[q] = (q < NS) ? nv.C[cpv * NS + q] * m : 0.0;
         }
 #ifdef PCK_TRACE
-        const bool tr = (x.cidx == pck_trace_cond) && x.gl == 0;
         const double ymin = gmin<G>(x.row ? y : INFINITY);
         auto trace = [&](double q, double luok) {
             if (!tr) return;
@@ -440,22 +457,25 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
 #else
         auto trace = [&](double, double) {};
 #endif
-        if (!grp_lu<NSP, G>(x, F)) {
+        bool luok;
+        PCK_PH(1, (luok = grp_lu<NSP, G>(x, F)));
+        if (!luok) {
             trace(-1.0, 0.0);
             h *= 0.25;
             if (!(h > 2.220446049250313e-15 * fmax(fabs(t), 1e-300))) return PCK_ST_STEPFAIL;
             continue;
         }
-        const double k1 = grp_solve<NSP, G>(x, F, keep * F0);
-        double fu = grp_rhs<NSP, G>(gv, x, y + a21 * k1);
-        const double k2 = grp_solve<NSP, G>(x, F, keep * (fu + ih * (C21 * k1)));
-        fu = grp_rhs<NSP, G>(gv, x, y + a31 * k1 + a32 * k2);
-        const double k3 = grp_solve<NSP, G>(x, F, keep * (fu + ih * (C31 * k1 + C32 * k2)));
-        fu = grp_rhs<NSP, G>(gv, x, y + a41 * k1 + a42 * k2 + a43 * k3);
-        const double k4 = grp_solve<NSP, G>(x, F, keep * (fu + ih * (C41 * k1 + C42 * k2 + C43 * k3)));
-        double u = y + a51 * k1 + a52 * k2 + a53 * k3 + a54 * k4;
-        fu = grp_rhs<NSP, G>(gv, x, u);
-        const double k5 = grp_solve<NSP, G>(x, F, keep * (fu + ih * (C51 * k1 + C52 * k2 + C53 * k3 + C54 * k4)));
+        double k1, k2, k3, k4, k5, k6, fu, u;
+        PCK_PH(2, (k1 = grp_solve<NSP, G>(x, F, keep * F0)));
+        PCK_PH(3, (fu = grp_rhs<NSP, G>(gv, x, y + a21 * k1)));
+        PCK_PH(2, (k2 = grp_solve<NSP, G>(x, F, keep * (fu + ih * (C21 * k1)))));
+        PCK_PH(3, (fu = grp_rhs<NSP, G>(gv, x, y + a31 * k1 + a32 * k2)));
+        PCK_PH(2, (k3 = grp_solve<NSP, G>(x, F, keep * (fu + ih * (C31 * k1 + C32 * k2)))));
+        PCK_PH(3, (fu = grp_rhs<NSP, G>(gv, x, y + a41 * k1 + a42 * k2 + a43 * k3)));
+        PCK_PH(2, (k4 = grp_solve<NSP, G>(x, F, keep * (fu + ih * (C41 * k1 + C42 * k2 + C43 * k3)))));
+        u = y + a51 * k1 + a52 * k2 + a53 * k3 + a54 * k4;
+        PCK_PH(3, (fu = grp_rhs<NSP, G>(gv, x, u)));
+        PCK_PH(2, (k5 = grp_solve<NSP, G>(x, F, keep * (fu + ih * (C51 * k1 + C52 * k2 + C53 * k3 + C54 * k4)))));
         double d2 = 0.0, d3 = 0.0;                 // dense output (mk_solver.h: rodas4_dense)
         if constexpr (TRAJ) {
             using namespace rodas4_dense;
@@ -463,9 +483,9 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
             d3 = D31 * k1 + D32 * k2 + D33 * k3 + D34 * k4 + D35 * k5;
         }
         u += k5;
-        fu = grp_rhs<NSP, G>(gv, x, u);
-        const double k6 = grp_solve<NSP, G>(x, F, keep * (fu + ih * (C61 * k1 + C62 * k2 + C63 * k3 + C64 * k4 +
-                                                                     C65 * k5)));
+        PCK_PH(3, (fu = grp_rhs<NSP, G>(gv, x, u)));
+        PCK_PH(2, (k6 = grp_solve<NSP, G>(x, F, keep * (fu + ih * (C61 * k1 + C62 * k2 + C63 * k3 + C64 * k4 +
+                                                                     C65 * k5)))));
         u += k6;
         const bool fin_l = !x.row || (isfinite(u) && isfinite(k6));
         const double fin = gmin<G>(fin_l ? 1.0 : 0.0);
@@ -473,17 +493,16 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
         const double r = k6 * __builtin_amdgcn_rcp(sc);     // error weight: the v_rcp_f64 estimate suffices
         const double s = gsum<G>(x.row ? r * r : 0.0);
         const double q = (fin > 0.0) ? s * invNS : INFINITY;     // en^2
-        // positivity (mass-action concentrations stay >= 0): a step that
+        // positivity (mass-action concentrations stay >= -atol): a step that
         // drives a component below -atol is rejected and retried at the
-        // fraction of the step where that component reaches -atol; accepted
-        // states are clipped at 0, so a component never sits below zero
+        // fraction of the step where that component reaches -atol
         const double pf = gmin<G>((x.row && u < -atol) ? (y + atol) / (y - u) : 1.0);
         const double fac = step_factor(q);
         trace(q, 1.0);
         if (q <= 1.0 && pf >= 1.0) {
             const double t_old = t, y_old = y;
             t = last ? t_end : t + h;
-            y = x.row ? fmax(u, 0.0) : 0.0;        // tolerance-level negatives (>= -atol) to 0
+            y = x.row ? u : 0.0;
 #pragma unroll
             for (int l = 0; l < PCK_MAX_CONS; ++l) {
                 if (l < nv.NCONS) {
@@ -502,7 +521,13 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
                             y_old * s1 + sv * (y + s1 * (d2 + sv * d3));
                 }
             }
-            F0 = grp_rhs<NSP, G>(gv, x, y);
+            PCK_PH(3, (F0 = grp_rhs<NSP, G>(gv, x, y)));
+            // falling tolerance-level negatives to 0 (mk_solver.h: integrate)
+            const bool negf = x.row && y < 0.0 && F0 < 0.0;
+            if (gmaxi<G>(negf ? 1 : 0) > 0) {
+                if (negf) y = 0.0;
+                PCK_PH(3, (F0 = grp_rhs<NSP, G>(gv, x, y)));
+            }
             h *= fmin(6.0, fmax(0.2, fac));
         } else if (q <= 1.0) {
             h *= fmax(0.1, 0.9 * pf);

@@ -148,6 +148,13 @@ extern "C" int pck_trace_set(long long cond) {
     int zero = 0;
     HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(pck_trace_cond), &cond, sizeof(cond)));
     HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(pck_trace_pos), &zero, sizeof(zero)));
+    const double ph0[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(pck_phase), ph0, sizeof(ph0)));
+    return PCK_OK;
+}
+extern "C" int pck_phase_get(double* host8) {
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpyFromSymbol(host8, HIP_SYMBOL(pck_phase), sizeof(double) * 8));
     return PCK_OK;
 }
 extern "C" int pck_trace_get(double* host, int* pos) {
@@ -489,14 +496,21 @@ static bool use_group(const pck_network* net, int lanes_per_cond) {
 // Lane-group kernels: compiled-in sizes <NSP, G, P> (NS <= NSP) and the
 // exact-size specialisation hipRTC compiles at the first solve (mk_jit.h).
 static inline int grp_g(int NS) { return NS <= 16 ? 16 : NS <= 32 ? 32 : 64; }
-// Jacobian column passes: keep the group's J block near 6 KiB of LDS
-static inline int grp_p(int NS) { const int b = NS * NS * 8; return b <= 6144 ? 1 : b <= 12288 ? 2 : 4; }
+// Jacobian column passes: the whole NS x NS block in LDS (one pass, 20 KiB
+// at NS = 50) -- measured 2.3x faster per Jacobian than 4 passes over a
+// 6 KiB block at NS = 50 (tools/phase_group.py).  PCK_GRP_PASSES=n forces
+// n passes (A/B).
+static inline int grp_p(int NS) {
+    const char* e = getenv("PCK_GRP_PASSES");
+    const int p = e ? atoi(e) : 1;
+    return (p >= 1 && p <= NS) ? p : 1;
+}
 #define PCK_GRP_SWITCH(NS, CALL)              \
     if ((NS) <= 16) { CALL(16, 16, 1); }       \
-    else if ((NS) <= 32) { CALL(32, 32, 2); }  \
-    else { CALL(64, 64, 4); }
+    else if ((NS) <= 32) { CALL(32, 32, 1); }  \
+    else { CALL(64, 64, 1); }
 static inline int grp_nsp_ct(int NS) { return NS <= 16 ? 16 : NS <= 32 ? 32 : 64; }
-static inline int grp_p_ct(int NS) { return NS <= 16 ? 1 : NS <= 32 ? 2 : 4; }
+static inline int grp_p_ct(int) { return 1; }
 
 static int grp_shape(const pck_network* net, int nsp, int P, size_t* shm, int* QB) {
     const int NS = net->nv.NDYN;

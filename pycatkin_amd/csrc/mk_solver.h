@@ -452,10 +452,9 @@ __device__ __forceinline__ int integrate(const P& p, const Lane<P::NS>& L, const
             s += r * r;
         }
         const double q = finite ? s * (1.0 / NS) : INFINITY;    // en^2
-        // positivity (mass-action concentrations stay >= 0): a step that
+        // positivity (mass-action concentrations stay >= -atol): a step that
         // drives a component below -atol is rejected and retried at the
-        // fraction of the step where that component reaches -atol; accepted
-        // states are clipped at 0, so a component never sits below zero
+        // fraction of the step where that component reaches -atol
         bool negv = false;
 #pragma unroll
         for (int i = 0; i < NS; ++i) negv = negv || (u[i] < -atol);
@@ -475,7 +474,7 @@ __device__ __forceinline__ int integrate(const P& p, const Lane<P::NS>& L, const
                 for (int i = 0; i < NS; ++i) y_old[i] = y[i];
             }
 #pragma unroll
-            for (int i = 0; i < NS; ++i) y[i] = fmax(u[i], 0.0);     // tolerance-level negatives (>= -atol) to 0
+            for (int i = 0; i < NS; ++i) y[i] = u[i];
             // Rosenbrock stages keep linear invariants only up to the rounding of
             // the stiff LU; rescale each non-negative site balance back onto its
             // initial total (multiplicative, so tiny coverages keep their digits)
@@ -505,6 +504,21 @@ __device__ __forceinline__ int integrate(const P& p, const Lane<P::NS>& L, const
                 }
             }
             rhs(p, L, k, y, F0);
+            // a tolerance-level negative (>= -atol) that is still falling is set
+            // to 0: left alone, a mass-action term of order >= 2 keeps driving it
+            // down and the positivity rule then shrinks h to nothing; clipping
+            // every negative instead perturbs the stiff modes at each step and
+            // the error estimate rejects steps forever (tools/rodas_mirror.py
+            // CLIPMODE, DESIGN.md "Positivity")
+            bool negf = false;
+#pragma unroll
+            for (int i = 0; i < NS; ++i) negf = negf || (y[i] < 0.0 && F0[i] < 0.0);
+            if (__any(negf)) {      // rare: one wave-uniform branch
+#pragma unroll
+                for (int i = 0; i < NS; ++i)
+                    if (y[i] < 0.0 && F0[i] < 0.0) y[i] = 0.0;
+                rhs(p, L, k, y, F0);
+            }
             h *= fmin(6.0, fmax(0.2, fac));
         } else if (q <= 1.0) {
             h *= fmax(0.1, 0.9 * pf);

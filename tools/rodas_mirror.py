@@ -155,7 +155,8 @@ def rodas4(f, J, y, t0, t_end, rtol, atol, cons=None, max_steps=200000, cons_row
         if acc:
             t_old, y_old = t, y
             t = t_end if last else t + h
-            y = unew if os.environ.get('NOCLIP') else np.maximum(unew, 0.0)
+            cm = os.environ.get('CLIPMODE', 'noclip' if os.environ.get('NOCLIP') else 'clip')
+            y = np.maximum(unew, 0.0) if cm == 'clip' else unew
             if cons is not None:
                 for l in range(cons.shape[0]):
                     if np.all(cons[l] >= 0):
@@ -171,6 +172,11 @@ def rodas4(f, J, y, t0, t_end, rtol, atol, cons=None, max_steps=200000, cons_row
                     samples.append(y_old * s1 + s * (y + s1 * (d2 + s * d3)))
                     ko += 1
             F0 = f(y)
+            if cm == 'hybrid':                 # clip only components that are negative and still falling
+                neg = (y < 0.0) & (F0 < 0.0)
+                if np.any(neg):
+                    y = np.where(neg, 0.0, y)
+                    F0 = f(y)
             h *= min(6.0, max(0.2, fac))
         else:
             h *= max(0.2, fac) if fin else 0.25
