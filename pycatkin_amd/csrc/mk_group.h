@@ -79,30 +79,81 @@ __device__ __forceinline__ void wsync() {
     __builtin_amdgcn_wave_barrier();
 }
 
+// Group all-reductions.  Within each row of 16 lanes: xor-1 / xor-2 by DPP
+// quad_perm, then row_half_mirror and row_mirror (4 DPP steps, no LDS); a
+// 32- or 64-lane group then combines its rows' results read with v_readlane
+// (uniform).  Every lane of a group gets the bitwise-same value (the same
+// operands in the same order), so control flow on the result stays
+// group-uniform.  Callers reduce at group-uniform points only: every lane of
+// the group is active.
+template <int CTRL>
+__device__ __forceinline__ double dppd(double v) { return __builtin_amdgcn_update_dpp(v, v, CTRL, 0xf, 0xf, false); }
+template <int CTRL>
+__device__ __forceinline__ int dppi(int v) { return __builtin_amdgcn_update_dpp(v, v, CTRL, 0xf, 0xf, false); }
+__device__ __forceinline__ double rlane(double v, int l) {
+    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l),
+                            __builtin_amdgcn_readlane(__double2loint(v), l));
+}
+
+#define PCK_ROW_REDUCE(v, OP, DPP)  \
+    v = OP(v, DPP<0xB1>(v));       /* quad_perm [1,0,3,2] */ \
+    v = OP(v, DPP<0x4E>(v));       /* quad_perm [2,3,0,1] */ \
+    v = OP(v, DPP<0x141>(v));      /* row_half_mirror */     \
+    v = OP(v, DPP<0x140>(v))       /* row_mirror */
+
+__device__ __forceinline__ double rlane_t(double v, int l) { return rlane(v, l); }
+__device__ __forceinline__ int rlane_t(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+
+template <int G, class T, class F>
+__device__ __forceinline__ T grows(T v, F op) {
+    if constexpr (G == 64) {
+        const T a = rlane_t(v, 0), b = rlane_t(v, 16), c = rlane_t(v, 32), d = rlane_t(v, 48);
+        return op(op(a, b), op(c, d));
+    } else if constexpr (G == 32) {
+        const T a = rlane_t(v, 0), b = rlane_t(v, 16), c = rlane_t(v, 32), d = rlane_t(v, 48);
+        return (threadIdx.x & 32) ? op(c, d) : op(a, b);
+    } else {
+        return v;
+    }
+}
+
+__device__ __forceinline__ double op_add(double a, double b) { return a + b; }
+__device__ __forceinline__ double op_max(double a, double b) { return fmax(a, b); }
+__device__ __forceinline__ double op_min(double a, double b) { return fmin(a, b); }
+__device__ __forceinline__ int op_maxi(int a, int b) { return max(a, b); }
+
 template <int G>
 __device__ __forceinline__ double gsum(double v) {
-#pragma unroll
-    for (int m = G / 2; m >= 1; m >>= 1) v += __shfl_xor(v, m, G);
-    return v;
+    PCK_ROW_REDUCE(v, op_add, dppd);
+    return grows<G>(v, op_add);
 }
 template <int G>
 __device__ __forceinline__ double gmax(double v) {
-#pragma unroll
-    for (int m = G / 2; m >= 1; m >>= 1) v = fmax(v, __shfl_xor(v, m, G));
-    return v;
+    PCK_ROW_REDUCE(v, op_max, dppd);
+    return grows<G>(v, op_max);
 }
 template <int G>
 __device__ __forceinline__ double gmin(double v) {
-#pragma unroll
-    for (int m = G / 2; m >= 1; m >>= 1) v = fmin(v, __shfl_xor(v, m, G));
-    return v;
+    PCK_ROW_REDUCE(v, op_min, dppd);
+    return grows<G>(v, op_min);
 }
 template <int G>
 __device__ __forceinline__ int gmaxi(int v) {
-#pragma unroll
-    for (int m = G / 2; m >= 1; m >>= 1) v = max(v, __shfl_xor(v, m, G));
-    return v;
+    PCK_ROW_REDUCE(v, op_maxi, dppi);
+    return grows<G>(v, op_maxi);
 }
+
+// lane K (compile-time after unrolling) of every row of 16: DPP row_newbcast
+__device__ __forceinline__ double bc16(double v, int k) {
+    switch (k) {
+#define PCK_BC(K) case K: return __builtin_amdgcn_update_dpp(0.0, v, 0x150 + K, 0xf, 0xf, false);
+        PCK_BC(0) PCK_BC(1) PCK_BC(2) PCK_BC(3) PCK_BC(4) PCK_BC(5) PCK_BC(6) PCK_BC(7)
+        PCK_BC(8) PCK_BC(9) PCK_BC(10) PCK_BC(11) PCK_BC(12) PCK_BC(13) PCK_BC(14) PCK_BC(15)
+#undef PCK_BC
+        default: return 0.0;
+    }
+}
+
 // broadcast lane `src` (group-uniform) of the group
 template <int G>
 __device__ __forceinline__ double gbcast(double v, int src) {
@@ -287,13 +338,81 @@ struct LU {
     double W[NSP];
     Perm<NSP> pk;
     int step;
+    int src;        // 16-lane groups (physical row swaps): original row now held by this lane
 };
+
+// 16-lane groups (one row of the wavefront per condition): LU with partial
+// pivoting by PHYSICAL row interchanges, so the pivot row of column k always
+// sits in lane k and every broadcast has a compile-time source lane: DPP
+// row_newbcast (one v_mov_b64_dpp, no LDS, no barrier).  The interchange
+// itself moves both rows' registers with ds_bpermute, only in waves where
+// some group swaps (wave vote).  Same pivots and the same operations in the
+// same order as the lane-indexed form below: identical factors.
+template <int NSP>
+__device__ __forceinline__ bool grp_lu16(const Grp<NSP>& x, LU<NSP>& F) {
+    bool ok = true;
+    F.src = x.gl;
+#pragma unroll
+    for (int k = 0; k < NSP; ++k) {
+        if (k < x.NS) {
+            const float mag = (float)fabs(F.W[k]);
+            int key = (x.row && x.gl >= k) ? (int)((__float_as_uint(mag) & ~63u) | (uint32_t)x.gl) : -1;
+            key = gmaxi<16>(key);
+            const int p = key & 63;
+            ok = ok && key >= 0;
+            if (__any(p != k)) {
+                const int from = (x.gl == k) ? p : (x.gl == p) ? k : x.gl;
+#pragma unroll
+                for (int j = 0; j < NSP; ++j) F.W[j] = __shfl(F.W[j], from, 16);
+                F.src = __shfl(F.src, from, 16);
+            }
+            const double piv = bc16(F.W[k], k);
+            ok = ok && piv != 0.0 && isfinite(piv);
+            const double inv = rcp(piv);
+            const bool below = x.gl > k;            // padding lanes hold zero rows: updates are no-ops
+            const double l = F.W[k] * inv;
+            if (x.gl == k) F.W[k] = inv;
+            if (below) F.W[k] = l;
+#pragma unroll
+            for (int j = k + 1; j < NSP; ++j) {
+                if (j < x.NS) {
+                    const double pj = bc16(F.W[j], k);
+                    if (below) F.W[j] = fma(-l, pj, F.W[j]);
+                }
+            }
+        }
+    }
+    return ok;
+}
+
+template <int NSP>
+__device__ __forceinline__ double grp_solve16(const Grp<NSP>& x, const LU<NSP>& F, double b) {
+    b = __shfl(b, F.src, 16);                      // the row interchanges of the factorisation
+#pragma unroll
+    for (int k = 0; k < NSP; ++k) {
+        if (k < x.NS) {
+            const double bk = bc16(b, k);
+            if (x.gl > k) b = fma(-F.W[k], bk, b);
+        }
+    }
+#pragma unroll
+    for (int kk = 0; kk < NSP; ++kk) {
+        const int k = NSP - 1 - kk;
+        if (k < x.NS) {
+            const double xk = bc16(b * F.W[k], k);
+            if (x.gl < k) b = fma(-F.W[k], xk, b);
+            if (x.gl == k) b = xk;
+        }
+    }
+    return x.row ? b : 0.0;
+}
 
 #ifndef PCK_GRP_READLANE
 #define PCK_GRP_READLANE 1
 #endif
 template <int NSP, int G>
 __device__ __forceinline__ bool grp_lu(const Grp<NSP>& x, LU<NSP>& F) {
+    if constexpr (G == 16 && NSP <= 16) return grp_lu16<NSP>(x, F);
     bool fre = x.row;
     bool ok = true;
     F.step = NSP;
@@ -353,6 +472,7 @@ __device__ __forceinline__ bool grp_lu(const Grp<NSP>& x, LU<NSP>& F) {
 // Solve (LU) x = b for the group; b_i on lane i in, x_i on lane i out.
 template <int NSP, int G>
 __device__ __forceinline__ double grp_solve(const Grp<NSP>& x, const LU<NSP>& F, double b) {
+    if constexpr (G == 16 && NSP <= 16) return grp_solve16<NSP>(x, F, b);
 #pragma unroll
     for (int k = 0; k < NSP; ++k) {
         if (k < x.NS) {
@@ -496,7 +616,7 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
         // positivity (mass-action concentrations stay >= -atol): a step that
         // drives a component below -atol is rejected and retried at the
         // fraction of the step where that component reaches -atol
-        const double pf = gmin<G>((x.row && u < -atol) ? (y + atol) / (y - u) : 1.0);
+        const double pf = PCK_POSITIVITY ? gmin<G>((x.row && u < -atol) ? (y + atol) / (y - u) : 1.0) : 1.0;
         const double fac = step_factor(q);
         trace(q, 1.0);
         if (q <= 1.0 && pf >= 1.0) {
@@ -524,7 +644,7 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
             PCK_PH(3, (F0 = grp_rhs<NSP, G>(gv, x, y)));
             // falling tolerance-level negatives to 0 (mk_solver.h: integrate)
             const bool negf = x.row && y < 0.0 && F0 < 0.0;
-            if (gmaxi<G>(negf ? 1 : 0) > 0) {
+            if (PCK_POSITIVITY && gmaxi<G>(negf ? 1 : 0) > 0) {
                 if (negf) y = 0.0;
                 PCK_PH(3, (F0 = grp_rhs<NSP, G>(gv, x, y)));
             }

@@ -271,6 +271,20 @@ __device__ __forceinline__ void cons_zero(const P& p, double (&b)[NS]) {
 // run) keeps h above 2e-5 t.
 #define PCK_STALL_STEPS 16384
 #define PCK_STALL_H 1e-5
+#define PCK_STALL_EVERY 64       // lane solver: tested every 64th step (power of 2)
+// Positivity rule (reject steps that drive a component below -atol, clip
+// falling tolerance-level negatives to 0): PCK_POSITIVITY=1.  Off, the
+// integrator is plain Rodas4 like the reference's scipy BDF, which has no
+// such rule.
+#ifndef PCK_POSITIVITY
+#define PCK_POSITIVITY 1
+#endif
+// Conservation rows in the lane solver's stage systems (cons_rows below): an
+// A/B knob, compiled out by default (the runtime flag costs 3 % of the
+// volcano step); the lane-group solver reads PCK_CONS_ROWS=1 at run time.
+#ifndef PCK_CONS_ROWS
+#define PCK_CONS_ROWS 0
+#endif
 
 namespace rodas4 {
 constexpr double g = 0.25;
@@ -371,7 +385,7 @@ __device__ __forceinline__ int integrate(const P& p, const Lane<P::NS>& L, const
     int blowups = 0;
     int stall = 0;
     while (t < t_end) {
-        if (nsteps >= max_steps) return PCK_ST_MAXSTEPS;
+        if (__builtin_amdgcn_readfirstlane(nsteps) >= max_steps) return PCK_ST_MAXSTEPS;
         ++nsteps;
         bool last = false;
         if (t + h >= t_end) { h = t_end - t; last = true; }
@@ -384,7 +398,7 @@ __device__ __forceinline__ int integrate(const P& p, const Lane<P::NS>& L, const
             for (int q = 0; q < NS; ++q) W[i][q] = -W[i][q];
             W[i][i] += ig;
         }
-        if (crows) cons_rows(p, W);
+        if (PCK_CONS_ROWS && crows) cons_rows(p, W);
         if (!lu<NS>(W, piv, sw)) {
             h *= 0.25;
             if (!(h > 2.220446049250313e-15 * fmax(fabs(t), 1e-300))) return PCK_ST_STEPFAIL;
@@ -393,35 +407,35 @@ __device__ __forceinline__ int integrate(const P& p, const Lane<P::NS>& L, const
         double k1[NS], k2[NS], k3[NS], k4[NS], k5[NS], u[NS], fu[NS];
 #pragma unroll
         for (int i = 0; i < NS; ++i) k1[i] = F0[i];
-        if (crows) cons_zero(p, k1);
+        if (PCK_CONS_ROWS && crows) cons_zero(p, k1);
         lu_solve<NS>(W, piv, sw, k1);
 #pragma unroll
         for (int i = 0; i < NS; ++i) u[i] = y[i] + a21 * k1[i];
         rhs(p, L, k, u, fu);
 #pragma unroll
         for (int i = 0; i < NS; ++i) k2[i] = fu[i] + ih * (C21 * k1[i]);
-        if (crows) cons_zero(p, k2);
+        if (PCK_CONS_ROWS && crows) cons_zero(p, k2);
         lu_solve<NS>(W, piv, sw, k2);
 #pragma unroll
         for (int i = 0; i < NS; ++i) u[i] = y[i] + a31 * k1[i] + a32 * k2[i];
         rhs(p, L, k, u, fu);
 #pragma unroll
         for (int i = 0; i < NS; ++i) k3[i] = fu[i] + ih * (C31 * k1[i] + C32 * k2[i]);
-        if (crows) cons_zero(p, k3);
+        if (PCK_CONS_ROWS && crows) cons_zero(p, k3);
         lu_solve<NS>(W, piv, sw, k3);
 #pragma unroll
         for (int i = 0; i < NS; ++i) u[i] = y[i] + a41 * k1[i] + a42 * k2[i] + a43 * k3[i];
         rhs(p, L, k, u, fu);
 #pragma unroll
         for (int i = 0; i < NS; ++i) k4[i] = fu[i] + ih * (C41 * k1[i] + C42 * k2[i] + C43 * k3[i]);
-        if (crows) cons_zero(p, k4);
+        if (PCK_CONS_ROWS && crows) cons_zero(p, k4);
         lu_solve<NS>(W, piv, sw, k4);
 #pragma unroll
         for (int i = 0; i < NS; ++i) u[i] = y[i] + a51 * k1[i] + a52 * k2[i] + a53 * k3[i] + a54 * k4[i];
         rhs(p, L, k, u, fu);
 #pragma unroll
         for (int i = 0; i < NS; ++i) k5[i] = fu[i] + ih * (C51 * k1[i] + C52 * k2[i] + C53 * k3[i] + C54 * k4[i]);
-        if (crows) cons_zero(p, k5);
+        if (PCK_CONS_ROWS && crows) cons_zero(p, k5);
         lu_solve<NS>(W, piv, sw, k5);
         double d2[TRAJ ? NS : 1], d3[TRAJ ? NS : 1];
         if constexpr (TRAJ) {
@@ -439,14 +453,15 @@ __device__ __forceinline__ int integrate(const P& p, const Lane<P::NS>& L, const
 #pragma unroll
         for (int i = 0; i < NS; ++i)
             k5[i] = fu[i] + ih * (C61 * k1[i] + C62 * k2[i] + C63 * k3[i] + C64 * k4[i] + C65 * k5[i]);
-        if (crows) cons_zero(p, k5);
+        if (PCK_CONS_ROWS && crows) cons_zero(p, k5);
         lu_solve<NS>(W, piv, sw, k5);
         bool finite = true;
-        double s = 0.0;
+        double s = 0.0, umin = INFINITY;
 #pragma unroll
         for (int i = 0; i < NS; ++i) {
             u[i] += k5[i];
             finite = finite && isfinite(u[i]) && isfinite(k5[i]);
+            umin = fmin(umin, u[i]);
             const double sc = atol + rtol * fmax(fabs(y[i]), fabs(u[i]));
             const double r = k5[i] * __builtin_amdgcn_rcp(sc);   // error weight: the v_rcp_f64 estimate suffices
             s += r * r;
@@ -455,17 +470,9 @@ __device__ __forceinline__ int integrate(const P& p, const Lane<P::NS>& L, const
         // positivity (mass-action concentrations stay >= -atol): a step that
         // drives a component below -atol is rejected and retried at the
         // fraction of the step where that component reaches -atol
-        bool negv = false;
-#pragma unroll
-        for (int i = 0; i < NS; ++i) negv = negv || (u[i] < -atol);
-        double pf = 1.0;
-        if (__any(negv)) {          // rare: one wave-uniform branch
-#pragma unroll
-            for (int i = 0; i < NS; ++i)
-                if (u[i] < -atol) pf = fmin(pf, (y[i] + atol) / (y[i] - u[i]));
-        }
+        const bool negv = PCK_POSITIVITY && umin < -atol;
         const double fac = step_factor(q);
-        if (q <= 1.0 && pf >= 1.0) {
+        if (q <= 1.0 && !negv) {
             const double t_old = t;
             t = last ? t_end : t + h;
             double y_old[TRAJ ? NS : 1];
@@ -509,26 +516,40 @@ __device__ __forceinline__ int integrate(const P& p, const Lane<P::NS>& L, const
             // down and the positivity rule then shrinks h to nothing; clipping
             // every negative instead perturbs the stiff modes at each step and
             // the error estimate rejects steps forever (tools/rodas_mirror.py
-            // CLIPMODE, DESIGN.md "Positivity")
-            bool negf = false;
+            // CLIPMODE, DESIGN.md "Positivity").  The common case costs one
+            // min over the state and one wave vote.
+            double ymin = y[0];
 #pragma unroll
-            for (int i = 0; i < NS; ++i) negf = negf || (y[i] < 0.0 && F0[i] < 0.0);
-            if (__any(negf)) {      // rare: one wave-uniform branch
+            for (int i = 1; i < NS; ++i) ymin = fmin(ymin, y[i]);
+            if (PCK_POSITIVITY && __any(ymin < 0.0)) {        // rare: one wave-uniform branch
+                bool negf = false;
 #pragma unroll
                 for (int i = 0; i < NS; ++i)
-                    if (y[i] < 0.0 && F0[i] < 0.0) y[i] = 0.0;
-                rhs(p, L, k, y, F0);
+                    if (y[i] < 0.0 && F0[i] < 0.0) { y[i] = 0.0; negf = true; }
+                if (__any(negf)) rhs(p, L, k, y, F0);
             }
             h *= fmin(6.0, fmax(0.2, fac));
-        } else if (q <= 1.0) {
-            h *= fmax(0.1, 0.9 * pf);
         } else {
-            h *= finite ? fmax(0.2, fac) : 0.25;
-            // repeated catastrophic rejections: see mk_group.h grp_integrate
-            if (!(q < PCK_BLOWUP_Q) && h < 1e-4 * t && ++blowups > PCK_MAX_BLOWUPS) return PCK_ST_STEPFAIL;
+            double pf = 1.0;
+            if (__any(negv)) {              // rare: one wave-uniform branch
+#pragma unroll
+                for (int i = 0; i < NS; ++i)
+                    if (u[i] < -atol) pf = fmin(pf, (y[i] + atol) / (y[i] - u[i]));
+            }
+            if (q <= 1.0) {
+                h *= fmax(0.1, 0.9 * pf);
+            } else {
+                h *= finite ? fmax(0.2, fac) : 0.25;
+                // repeated catastrophic rejections: see mk_group.h grp_integrate
+                if (!(q < PCK_BLOWUP_Q) && h < 1e-4 * t && ++blowups > PCK_MAX_BLOWUPS) return PCK_ST_STEPFAIL;
+            }
         }
-        stall = (h < PCK_STALL_H * (t - t0)) ? stall + 1 : 0;
-        if (stall > PCK_STALL_STEPS) return PCK_ST_STEPFAIL;
+        // stagnation, sampled every PCK_STALL_EVERY steps (the active lanes of a
+        // wave share the step counter: a scalar test)
+        if ((__builtin_amdgcn_readfirstlane(nsteps) & (PCK_STALL_EVERY - 1)) == 0) {
+            stall = (h < PCK_STALL_H * (t - t0)) ? stall + PCK_STALL_EVERY : 0;
+            if (stall > PCK_STALL_STEPS) return PCK_ST_STEPFAIL;
+        }
         // scipy's BDF limit: a step below 10 ulp(t) is a failure
         if (!(h > 2.220446049250313e-15 * fmax(fabs(t), 1e-300)) && t < t_end) return PCK_ST_STEPFAIL;
     }

@@ -176,3 +176,24 @@ def test_output_times_follow_the_reference_ode_grid():
     np.testing.assert_allclose(t, np.concatenate(([0.0], np.logspace(-8, np.log10(3600.0), 5))))
     s = P.System(times=[1.0, 1.0e4], nsteps=3)
     np.testing.assert_allclose(s.output_times(), [0.0, 1.0, 100.0, 1.0e4])
+
+
+@pytest.mark.parametrize('net', ['DMTM', 'COOxVolcano'])
+def test_species_jacobian_is_exact(inputs, net):
+    """The oracle's species_jacobian is the exact derivative of species_odes,
+    gas columns included (old_system.py:262-271 leaves bartoPa off those
+    columns; DESIGN.md 'Reference semantics: Jacobian')."""
+    spec = spec_of(inputs, net)
+    if net == 'COOxVolcano':
+        O.set_volcano_point(spec, -1.0, -1.0, None)
+    m = O.ClassicModel(spec)
+    rng = np.random.default_rng(1)
+    y = rng.uniform(0.05, 0.5, len(m.snames))
+    J = m.species_jacobian(y)
+    for q in range(len(y)):
+        hq = 1e-6 * y[q]
+        yp, ym = y.copy(), y.copy()
+        yp[q] += hq
+        ym[q] -= hq
+        fd = (m.species_odes(yp) - m.species_odes(ym)) / (2.0 * hq)
+        np.testing.assert_allclose(J[:, q], fd, rtol=1e-6, atol=1e-6 * (np.abs(J).max() + 1e-300))

@@ -5,6 +5,8 @@
 set -e
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 mkdir -p "$ROOT/pycatkin_amd/_ab"
+# the hipRTC kernels compile from the embedded headers: refresh them first
+(cd "$ROOT" && python3 -c "import __graft_entry__ as g; g.embed_rtc_sources()")
 while [ $# -ge 2 ]; do
   name=$1; flags=$2; shift 2
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fno-signed-zeros -shared -fPIC $flags -I"$ROOT/include" \

@@ -185,7 +185,7 @@ def rodas4(f, J, y, t0, t_end, rtol, atol, cons=None, max_steps=200000, cons_row
     return y, 0, n
 
 
-def synthetic_model(idx, n_total=16384):
+def synthetic_model(idx, n_total=65536):
     from _synth import spec_of
     from oracle import mk_oracle as O
     from pycatkin_amd.functions.synthetic import synthetic_network

@@ -78,5 +78,31 @@ def main():
     print('lane-sorted   %.0f  speedup %.3f  (lane_eff %.4f)' % (m2, base / m2, steps.sum() / (c2.sum() * 64)))
 
 
-if __name__ == '__main__':
+
+def two_phase(steps, cap, s1, sort2=False):
+    """phase 1: every lane runs at most s1 steps; phase 2: the unfinished
+    lanes, compacted (launch order, or sorted by remaining steps), run the
+    rest.  Returns (makespan1, makespan2, unfinished lanes)."""
+    pad = (-len(steps)) % 64
+    c1 = np.minimum(np.pad(steps, (0, pad)).reshape(-1, 64).max(axis=1), s1)
+    rem = steps[steps > s1] - s1
+    if sort2:
+        rem = np.sort(rem)[::-1]
+    pad2 = (-len(rem)) % 64
+    c2 = np.pad(rem, (0, pad2)).reshape(-1, 64).max(axis=1) if len(rem) else np.zeros(0)
+    return makespan(c1, cap), (makespan(c2, cap) if len(c2) else 0.0), len(rem)
+
+
+if __name__ == '__main__' and len(sys.argv) > 3:
+    steps = np.load(sys.argv[1]).astype(np.float64)
+    cap = float(sys.argv[2])
+    base = makespan(np.pad(steps, (0, (-len(steps)) % 64)).reshape(-1, 64).max(axis=1), cap)
+    for s1 in [int(x) for x in sys.argv[3].split(',')]:
+        for srt in (False, True):
+            a, b, k = two_phase(steps, cap, s1, srt)
+            print('s1 %4d sort2 %d: phase1 %.0f phase2 %.0f (%d lanes) total %.0f speedup %.3f'
+                  % (s1, srt, a, b, k, a + b, base / (a + b)))
+
+
+if __name__ == '__main__' and len(sys.argv) <= 3:
     main()
