@@ -72,7 +72,17 @@ struct GrpView {
     const int32_t* row;
     const uint4* ent;
     int ND;                  // total participants = size of the derivative buffer
+    int NE;                  // entries of the species CSR (= row[NS])
 };
+
+// The solver kernel copies the tables into LDS once per block (shared by the
+// block's groups): every rate / Jacobian evaluation walks them, and from LDS
+// each dependent record fetch costs an LDS round trip instead of an L1/L2 one.
+// Layout (16-byte units): rx[max(R,1)] | ent[max(NE,1)] | row[NS+1] (int32)
+__host__ __device__ inline size_t grp_tab_doubles(int R, int NE, int NS) {
+    const size_t b = 16 * (size_t)(R > 0 ? R : 1) + 16 * (size_t)(NE > 0 ? NE : 1) + 4 * (size_t)(NS + 1);
+    return (b + 15) / 16 * 2;
+}
 
 __device__ __forceinline__ void wsync() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -234,17 +244,39 @@ struct Grp {
     double cfi, rs, fl, in;   // this row's concentration factor, row scale, flow, inflow
 };
 
-template <int NSP>
+// For networks on 64-lane groups (more than 32 species), the transient
+// integration evaluates rates and Jacobian at the clamped state max(y, 0)
+// instead of the positivity rule of the smaller networks (PCK_GRP_CLAMP,
+// default on; the Newton polish and the TOF use the plain mass-action
+// equations, whose root the reference's least_squares finds): a species at zero then has no consumption
+// term, so tolerance-level negatives decay instead of feeding second-order
+// terms of the wrong sign.  Large stiff networks (the synthetic 50 x 150 one)
+// otherwise either oscillate around zero in sign-alternating steps (plain
+// Rodas4, like scipy BDF, which fails outright on some of the same
+// conditions) or chatter at h ~ 1e-8 t under a reject-below--atol rule; the
+// CPU mirror (tools/rodas_mirror.py CLAMP=1) and the GPU both solve those
+// conditions in ~1e3 steps with it.  Where every component is >= 0 it
+// changes nothing.
+// PCK_GRP_EXACT=1 (set by the hipRTC compile, csrc/mk_jit.h): NSP equals the
+// network's species count, so every `k < NS` guard folds away at compile time
+#ifndef PCK_GRP_EXACT
+#define PCK_GRP_EXACT 0
+#endif
+#ifndef PCK_GRP_CLAMP
+#define PCK_GRP_CLAMP 1
+#endif
+
+template <int NSP, bool CL = false>
 __device__ __forceinline__ void put_c(const Grp<NSP>& x, double y) {
     wsync();                                   // previous readers of c / d are done
-    if (x.row) x.c[x.gl] = x.cfi * y;
+    if (x.row) x.c[x.gl] = x.cfi * ((CL && PCK_GRP_CLAMP) ? fmax(y, 0.0) : y);
     wsync();
 }
 
 // f_i = rs_i * sum_r S_ir net_r + fl_i (in_i - y_i)   (row lanes; 0 elsewhere)
-template <int NSP, int G>
+template <int NSP, int G, bool CL = false>
 __device__ __forceinline__ double grp_rhs(const GrpView& g, const Grp<NSP>& x, double y) {
-    put_c(x, y);
+    put_c<NSP, CL>(x, y);
     for (int r = x.gl; r < x.R; r += G) x.d[r] = rec_rate(g.rx[r], x.kf[r], x.kr[r], x.c);
     wsync();
     double f = 0.0;
@@ -269,11 +301,11 @@ __device__ __forceinline__ double grp_rhs(const GrpView& g, const Grp<NSP>& x, d
 
 // W[q] = sgn * dF_i/dy_q + (q == i ? shift : 0), with dF/dy including the flow
 // diagonal (-fl_i); 0 on lanes without a row
-template <int NSP, int G, int P>
+template <int NSP, int G, int P, bool CL = false>
 __device__ __forceinline__ void grp_jac(const NetView& nv, const GrpView& g, const Grp<NSP>& x, double y, double sgn,
                                         double shift, double (&W)[NSP]) {
     constexpr int QB = (NSP + P - 1) / P;
-    put_c(x, y);
+    put_c<NSP, CL>(x, y);
     for (int r = x.gl; r < x.R; r += G) {
         const uint4 rec = g.rx[r];
         const int np = rx_np(rec), dp = rx_dptr(rec);
@@ -502,6 +534,7 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
                                              double t0, double t_end, double rtol, double atol, int max_steps,
                                              int& nsteps, bool crows, const TrajOut& to) {
     using namespace rodas4;
+    constexpr bool CLAMP = PCK_GRP_CLAMP && G == 64;    // see put_c
     const int NS = x.NS;
     int ko = 0;
     if constexpr (TRAJ) {                       // samples at or before t0: the initial state
@@ -512,7 +545,7 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
     nsteps = 0;
     const double span = t_end - t0;
     if (!(span > 0.0)) return PCK_ST_OK;
-    double F0 = grp_rhs<NSP, G>(gv, x, y);
+    double F0 = grp_rhs<NSP, G, CLAMP>(gv, x, y);
     double cons0[PCK_MAX_CONS];
     double ci[PCK_MAX_CONS];
     bool cpos[PCK_MAX_CONS];
@@ -531,7 +564,7 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
         const double d1 = sqrt(gsum<G>(x.row ? (F0 / sc) * (F0 / sc) : 0.0) * invNS);
         double h0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : 0.01 * d0 / d1;
         h0 = fmin(h0, span);
-        const double F1 = grp_rhs<NSP, G>(gv, x, y + h0 * F0);
+        const double F1 = grp_rhs<NSP, G, CLAMP>(gv, x, y + h0 * F0);
         const double q = (F1 - F0) / sc;
         const double d2 = sqrt(gsum<G>(x.row ? q * q : 0.0) * invNS) / h0;
         const double h1 = (d1 <= 1e-15 && d2 <= 1e-15) ? fmax(1e-6, h0 * 1e-3) : pow(0.01 / fmax(d1, d2), 0.2);
@@ -556,7 +589,7 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
         const bool tr = (x.cidx == pck_trace_cond) && x.gl == 0;
         if (tr) pck_phase[5] += 1.0;
 #endif
-        PCK_PH(0, (grp_jac<NSP, G, P>(nv, gv, x, y, -1.0, ig, F.W)));       // W = I/(h g) - J
+        PCK_PH(0, (grp_jac<NSP, G, P, CLAMP>(nv, gv, x, y, -1.0, ig, F.W)));       // W = I/(h g) - J
         if (cpv >= 0) {                                        // conservation rows (mk_solver.h: cons_rows)
             double m = 0.0;
 #pragma unroll
@@ -587,14 +620,14 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
         }
         double k1, k2, k3, k4, k5, k6, fu, u;
         PCK_PH(2, (k1 = grp_solve<NSP, G>(x, F, keep * F0)));
-        PCK_PH(3, (fu = grp_rhs<NSP, G>(gv, x, y + a21 * k1)));
+        PCK_PH(3, (fu = grp_rhs<NSP, G, CLAMP>(gv, x, y + a21 * k1)));
         PCK_PH(2, (k2 = grp_solve<NSP, G>(x, F, keep * (fu + ih * (C21 * k1)))));
-        PCK_PH(3, (fu = grp_rhs<NSP, G>(gv, x, y + a31 * k1 + a32 * k2)));
+        PCK_PH(3, (fu = grp_rhs<NSP, G, CLAMP>(gv, x, y + a31 * k1 + a32 * k2)));
         PCK_PH(2, (k3 = grp_solve<NSP, G>(x, F, keep * (fu + ih * (C31 * k1 + C32 * k2)))));
-        PCK_PH(3, (fu = grp_rhs<NSP, G>(gv, x, y + a41 * k1 + a42 * k2 + a43 * k3)));
+        PCK_PH(3, (fu = grp_rhs<NSP, G, CLAMP>(gv, x, y + a41 * k1 + a42 * k2 + a43 * k3)));
         PCK_PH(2, (k4 = grp_solve<NSP, G>(x, F, keep * (fu + ih * (C41 * k1 + C42 * k2 + C43 * k3)))));
         u = y + a51 * k1 + a52 * k2 + a53 * k3 + a54 * k4;
-        PCK_PH(3, (fu = grp_rhs<NSP, G>(gv, x, u)));
+        PCK_PH(3, (fu = grp_rhs<NSP, G, CLAMP>(gv, x, u)));
         PCK_PH(2, (k5 = grp_solve<NSP, G>(x, F, keep * (fu + ih * (C51 * k1 + C52 * k2 + C53 * k3 + C54 * k4)))));
         double d2 = 0.0, d3 = 0.0;                 // dense output (mk_solver.h: rodas4_dense)
         if constexpr (TRAJ) {
@@ -603,7 +636,7 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
             d3 = D31 * k1 + D32 * k2 + D33 * k3 + D34 * k4 + D35 * k5;
         }
         u += k5;
-        PCK_PH(3, (fu = grp_rhs<NSP, G>(gv, x, u)));
+        PCK_PH(3, (fu = grp_rhs<NSP, G, CLAMP>(gv, x, u)));
         PCK_PH(2, (k6 = grp_solve<NSP, G>(x, F, keep * (fu + ih * (C61 * k1 + C62 * k2 + C63 * k3 + C64 * k4 +
                                                                      C65 * k5)))));
         u += k6;
@@ -616,7 +649,7 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
         // positivity (mass-action concentrations stay >= -atol): a step that
         // drives a component below -atol is rejected and retried at the
         // fraction of the step where that component reaches -atol
-        const double pf = PCK_POSITIVITY ? gmin<G>((x.row && u < -atol) ? (y + atol) / (y - u) : 1.0) : 1.0;
+        const double pf = (PCK_POSITIVITY && !CLAMP) ? gmin<G>((x.row && u < -atol) ? (y + atol) / (y - u) : 1.0) : 1.0;
         const double fac = step_factor(q);
         trace(q, 1.0);
         if (q <= 1.0 && pf >= 1.0) {
@@ -641,12 +674,12 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
                             y_old * s1 + sv * (y + s1 * (d2 + sv * d3));
                 }
             }
-            PCK_PH(3, (F0 = grp_rhs<NSP, G>(gv, x, y)));
+            PCK_PH(3, (F0 = grp_rhs<NSP, G, CLAMP>(gv, x, y)));
             // falling tolerance-level negatives to 0 (mk_solver.h: integrate)
             const bool negf = x.row && y < 0.0 && F0 < 0.0;
-            if (PCK_POSITIVITY && gmaxi<G>(negf ? 1 : 0) > 0) {
+            if (PCK_POSITIVITY && !CLAMP && gmaxi<G>(negf ? 1 : 0) > 0) {
                 if (negf) y = 0.0;
-                PCK_PH(3, (F0 = grp_rhs<NSP, G>(gv, x, y)));
+                PCK_PH(3, (F0 = grp_rhs<NSP, G, CLAMP>(gv, x, y)));
             }
             h *= fmin(6.0, fmax(0.2, fac));
         } else if (q <= 1.0) {
@@ -747,7 +780,7 @@ __device__ __forceinline__ void grp_setup(const NetView& nv, const GrpView& gv, 
     const int r1 = R > 0 ? R : 1;
     x.gl = threadIdx.x % G;
     x.cidx = c;
-    x.NS = nv.NDYN;
+    x.NS = PCK_GRP_EXACT ? NSP : nv.NDYN;   // hipRTC kernels are instantiated at the network's exact size
     x.R = R;
     x.QB = QB;
     x.row = x.gl < x.NS;
@@ -815,21 +848,36 @@ __global__ void __launch_bounds__(64) k_solve_grp(NetView nv, GrpView gv, CondVi
     const int64_t v = (int64_t)blockIdx.x * (64 / G) + grp;
     const int64_t c = v / ga.M;
     const int q = (int)(v % ga.M);
+    const int R1 = nv.NRXN > 0 ? nv.NRXN : 1, NE1 = gv.NE > 0 ? gv.NE : 1;
+    GrpView gl = gv;                                // the tables, copied to LDS by the whole block (one wave)
+    {
+        uint4* trx = (uint4*)lds;
+        uint4* tent = trx + R1;
+        int32_t* trow = (int32_t*)(tent + NE1);
+        for (int i = threadIdx.x; i < nv.NRXN; i += 64) trx[i] = gv.rx[i];
+        for (int i = threadIdx.x; i < gv.NE; i += 64) tent[i] = gv.ent[i];
+        for (int i = threadIdx.x; i <= nv.NDYN; i += 64) trow[i] = gv.row[i];
+        wsync();
+        gl.rx = trx;
+        gl.ent = tent;
+        gl.row = trow;
+    }
     if (c >= cv.n) return;                          // group-uniform exit; no block barriers below
     int pj = -1;
     double pfac = 1.0;
     if (q > 0) { pj = (q - 1) >> 1; pfac = (q & 1) ? 1.0 + a.eps : 1.0 - a.eps; }
     Grp<NSP> x;
     double T;
-    grp_setup<NSP, G>(nv, gv, cv, c, kf, kr, ld_k, pj, pfac,
-                      lds + (size_t)grp * grp_lds_doubles(nv.NRXN, NSP, nv.NDYN, gv.ND, ga.QB), ga.QB, x, T);
+    grp_setup<NSP, G>(nv, gl, cv, c, kf, kr, ld_k, pj, pfac,
+                      lds + grp_tab_doubles(nv.NRXN, gv.NE, nv.NDYN) +
+                          (size_t)grp * grp_lds_doubles(nv.NRXN, NSP, nv.NDYN, gv.ND, ga.QB), ga.QB, x, T);
     double y = x.row ? cv.y0[x.gl * cv.ld_y0 + c * cv.s_y0] : 0.0;
     int ns = 0;
     TrajOut to{a.t_out, a.n_out, a.traj, a.ld_traj, c};
-    int st = grp_integrate<NSP, G, P, TRAJ>(nv, gv, x, y, a.t0, a.t_end, a.rtol, a.atol, a.max_steps, ns,
+    int st = grp_integrate<NSP, G, P, TRAJ>(nv, gl, x, y, a.t0, a.t_end, a.rtol, a.atol, a.max_steps, ns,
                                             a.cons_rows != 0, to);
-    if (st == PCK_ST_OK && a.newton) st = grp_newton<NSP, G, P>(nv, gv, x, y, a.newton_iters);
-    const double tof = grp_tof<NSP, G>(nv, gv, x, y);
+    if (st == PCK_ST_OK && a.newton) st = grp_newton<NSP, G, P>(nv, gl, x, y, a.newton_iters);
+    const double tof = grp_tof<NSP, G>(nv, gl, x, y);
     const bool fin = gmin<G>((!x.row || isfinite(y)) ? 1.0 : 0.0) > 0.0 && isfinite(tof);
     if (!fin && st == PCK_ST_OK) st = PCK_ST_NONFINITE;
     if (ga.M > 1) {

@@ -318,6 +318,7 @@ extern "C" int pck_network_create(const int32_t* ip, int64_t n_ip, const double*
         net->gv.ent = (const uint4*)(buf + brx);
         net->gv.row = (const int32_t*)(buf + brx + bent);
         net->gv.ND = ND;
+        net->gv.NE = row[NS];
     }
     // structural digest -> compiled-in plan (same bytes as network.py: structural_digest)
     {
@@ -512,11 +513,12 @@ static inline int grp_p(int NS) {
 static inline int grp_nsp_ct(int NS) { return NS <= 16 ? 16 : NS <= 32 ? 32 : 64; }
 static inline int grp_p_ct(int) { return 1; }
 
-static int grp_shape(const pck_network* net, int nsp, int P, size_t* shm, int* QB) {
+static int grp_shape(const pck_network* net, int nsp, int P, size_t* shm, int* QB, bool tables = false) {
     const int NS = net->nv.NDYN;
     const int per = 64 / grp_g(NS);
     *QB = (nsp + P - 1) / P;
     *shm = sizeof(double) * per * grp_lds_doubles(net->nv.NRXN, nsp, NS, net->gv.ND, *QB);
+    if (tables) *shm += sizeof(double) * grp_tab_doubles(net->nv.NRXN, net->gv.NE, NS);   // k_solve_grp
     if (*shm > 64 * 1024)
         return fail(PCK_E_SIZE, "lane-group solver: network needs %s%lld bytes of LDS per wavefront", "", (long long)*shm);
     return PCK_OK;
@@ -660,7 +662,7 @@ static int launch_solve(pck_network* net, const pck_conditions* cond, const pck_
         if (traj && !f) return fail(PCK_E_HIP, "hipRTC compile of the trajectory kernel failed%s", "");
         size_t shm;
         if (f) {
-            rc = grp_shape(net, NS, P, &shm, &ga.QB);
+            rc = grp_shape(net, NS, P, &shm, &ga.QB, true);
             if (rc) return rc;
             NetView nv = net->nv;
             GrpView gv = net->gv;
@@ -671,7 +673,7 @@ static int launch_solve(pck_network* net, const pck_conditions* cond, const pck_
             void* args[] = {&nv, &gv, &cv, &kfp, &krp, &ldk, &a, &ga};
             HIPCHK(hipModuleLaunchKernel(f, g.x, 1, 1, 64, 1, 1, (unsigned)shm, s, args, nullptr));
         } else {
-            rc = grp_shape(net, grp_nsp_ct(NS), grp_p_ct(NS), &shm, &ga.QB);
+            rc = grp_shape(net, grp_nsp_ct(NS), grp_p_ct(NS), &shm, &ga.QB, true);
             if (rc) return rc;
 #define CALL(NP, GG, PP) hipLaunchKernelGGL((k_solve_grp<NP, GG, PP>), g, dim3(64), shm, s, net->nv, net->gv, cview(cond), kf, kr, n, a, ga)
             PCK_GRP_SWITCH(NS, CALL)

@@ -36,6 +36,16 @@ def summarise(d):
             v['fetch_bytes'] = 2.0 * 1024.0 * v.get('FETCH_SIZE', 0.0)
             v['write_bytes'] = 1024.0 * v.get('WRITE_SIZE', 0.0)
             v['traffic_bytes'] = v['fetch_bytes'] + v['write_bytes']
+        if 'SQ_INSTS_VALU_FMA_F64' in v:
+            # fp64 FLOPs from the instruction counters (per wave instruction: 64
+            # lanes, FMA = 2): an upper bound, exec-masked lanes count as active
+            f64 = v.get('SQ_INSTS_VALU_ADD_F64', 0.0) + v.get('SQ_INSTS_VALU_MUL_F64', 0.0) + \
+                v['SQ_INSTS_VALU_FMA_F64'] + v.get('SQ_INSTS_VALU_TRANS_F64', 0.0)
+            v['f64_wave_insts'] = f64
+            v['f64_flops_counted'] = 64.0 * (v.get('SQ_INSTS_VALU_ADD_F64', 0.0) + v.get('SQ_INSTS_VALU_MUL_F64', 0.0) +
+                                             v.get('SQ_INSTS_VALU_TRANS_F64', 0.0) + 2.0 * v['SQ_INSTS_VALU_FMA_F64'])
+            if v.get('SQ_INSTS_VALU'):
+                v['f64_share_of_valu'] = f64 / v['SQ_INSTS_VALU']
     return dict(out)
 
 

@@ -215,12 +215,14 @@ def main():
     dyn = m.dyn
     full = m.y0.copy()
 
+    clamp = os.environ.get('CLAMP') is not None      # rates / Jacobian at max(y, 0)
+
     def f(y):
-        full[dyn] = y
+        full[dyn] = np.maximum(y, 0.0) if clamp else y
         return m.rhs(full)[dyn]
 
     def J(y):
-        full[dyn] = y
+        full[dyn] = np.maximum(y, 0.0) if clamp else y
         return m.jac(full)[np.ix_(dyn, dyn)]
     y0 = m.y0[dyn].copy()
     C = m.conservation()
