@@ -163,24 +163,27 @@ def log(msg):
     print('[bench] ' + msg, file=sys.stderr, flush=True)
 
 
-def profiled_traffic(kernel_name, tag):
-    """HBM bytes per launch of `kernel_name` from the committed rocprofv3 PMC
+def profiled_counters(kernel_name, tag):
+    """Per-launch PMC figures of `kernel_name` from the committed rocprofv3
     summary named in profiles/CURRENT (written by tools/pmc_summary.py from a
-    tools/profile.sh run of this bench, same workload `tag`), or (None, None)."""
+    tools/profile.sh run of this bench, same workload `tag`): (summary entry,
+    path) or ({}, None)."""
     cur = os.path.join(ROOT, 'profiles', 'CURRENT')
     if not os.path.isfile(cur):
-        return None, None
+        return {}, None
     f = os.path.join(ROOT, open(cur).read().strip(), 'summary.json')
     try:
         s = json.load(open(f))
     except (OSError, ValueError):
-        return None, None
-    want = kernel_name.replace('pck::', '').replace('nets::', '').replace(' ', '')
+        return {}, None
+    def norm(name):      # 'pck::k_solve<pck::PlanCT<pck::nets::Volcano>, false>' -> 'k_solve<PlanCT<Volcano>>'
+        return name.replace('pck::', '').replace('nets::', '').replace(' ', '').replace(',false', '')
+    want = norm(kernel_name)
     for k, v in s.items():
-        short = k.replace('pck::', '').replace('nets::', '').replace(' ', '')
+        short = norm(k)
         if short == want and 'traffic_bytes' in v and v.get('tag', tag) == tag:
-            return v['traffic_bytes'], os.path.relpath(f, ROOT)
-    return None, None
+            return v, os.path.relpath(f, ROOT)
+    return {}, None
 
 
 # ----------------------------------------------------------------------------
@@ -578,16 +581,24 @@ def main(argv=None):
         roof, cpu_line = None, None
         if not cpu:
             fps = flops_per_step(wl.plan)
-            fl = fps * steps_local
+            fl_struct = fps * steps_local
+            pmc, traffic_src = profiled_counters(wl.kernel_name, wl.tag) if world == 1 else ({}, None)
+            traffic = pmc.get('traffic_bytes')
+            # the smaller of the structural count and the fp64 instruction
+            # counters of the committed profile of this same workload (which
+            # count exec-masked lanes too, so they are an upper bound themselves)
+            fl_pmc = pmc.get('f64_flops_counted')
+            fl = min(fl_struct, fl_pmc) if fl_pmc else fl_struct
             achieved = fl / (k3_ms * 1e-3) / 1e12
-            traffic, traffic_src = profiled_traffic(wl.kernel_name, wl.tag)
             roof = {'bound': 'mfma' if False else 'valu_fp64', 'achieved': achieved, 'peak': FP64_VECTOR_PEAK_TFLOPS,
                     'unit': 'TFLOP/s', 'frac': achieved / FP64_VECTOR_PEAK_TFLOPS, 'traffic': traffic,
                     'traffic_unit': 'bytes per launch (rocprofv3 PMC FETCH_SIZE x2 + WRITE_SIZE)',
                     'traffic_source': traffic_src, 'algorithmic_bytes': wl.algo_bytes,
                     'kernel': wl.kernel_name, 'kernel_ms': k3_ms, 'rate_constants_ms': k1_ms,
-                    'flops_per_launch': fl, 'flops_per_step': fps, 'flop_count': 'structural nonzeros of one '
-                    'accepted Rodas4 step x integrator steps of rank 0 (Newton polish, kernel 1 and TOF not counted)',
+                    'flops_per_launch': fl, 'flops_structural': fl_struct, 'flops_pmc_f64': fl_pmc,
+                    'flops_per_step': fps, 'flop_count': 'min(structural nonzeros of one accepted Rodas4 step x '
+                    'integrator steps of rank 0 (Newton polish, kernel 1 and TOF not counted), 64 x (ADD+MUL+TRANS) '
+                    '+ 128 x FMA fp64 wave instructions of the committed PMC profile of this workload)',
                     'integrator_steps': steps_local, 'lane_efficiency': lane_eff}
             if world == 1 and not args.no_cpu_baseline:
                 workers = min(16, os.cpu_count() or 1)

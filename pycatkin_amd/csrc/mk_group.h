@@ -75,9 +75,11 @@ struct GrpView {
     int NE;                  // entries of the species CSR (= row[NS])
 };
 
-// The solver kernel copies the tables into LDS once per block (shared by the
-// block's groups): every rate / Jacobian evaluation walks them, and from LDS
-// each dependent record fetch costs an LDS round trip instead of an L1/L2 one.
+// The solver kernel (TAB = true) copies the tables into LDS once per block
+// (shared by the block's groups): every rate / Jacobian evaluation walks
+// them, and from LDS each dependent record fetch costs an LDS round trip
+// instead of an L1/L2 one.  The host picks TAB only where the extra LDS does
+// not lower the kernel's occupancy (csrc/mk_kernels.hip: grp_tables_pay).
 // Layout (16-byte units): rx[max(R,1)] | ent[max(NE,1)] | row[NS+1] (int32)
 __host__ __device__ inline size_t grp_tab_doubles(int R, int NE, int NS) {
     const size_t b = 16 * (size_t)(R > 0 ? R : 1) + 16 * (size_t)(NE > 0 ? NE : 1) + 4 * (size_t)(NS + 1);
@@ -840,7 +842,7 @@ struct GrpArgs {
     int32_t* nsbuf;     // DRC mode: [M][n] integrator steps per perturbation
 };
 
-template <int NSP, int G, int P, bool TRAJ = false>
+template <int NSP, int G, int P, bool TRAJ = false, bool TAB = false>
 __global__ void __launch_bounds__(64) k_solve_grp(NetView nv, GrpView gv, CondView cv, const double* kf,
                                                   const double* kr, int64_t ld_k, SolveArgs a, GrpArgs ga) {
     extern __shared__ double lds[];
@@ -849,8 +851,8 @@ __global__ void __launch_bounds__(64) k_solve_grp(NetView nv, GrpView gv, CondVi
     const int64_t c = v / ga.M;
     const int q = (int)(v % ga.M);
     const int R1 = nv.NRXN > 0 ? nv.NRXN : 1, NE1 = gv.NE > 0 ? gv.NE : 1;
-    GrpView gl = gv;                                // the tables, copied to LDS by the whole block (one wave)
-    {
+    GrpView gl = gv;                                // TAB: the tables, copied to LDS by the whole block (one wave)
+    if constexpr (TAB) {
         uint4* trx = (uint4*)lds;
         uint4* tent = trx + R1;
         int32_t* trow = (int32_t*)(tent + NE1);
@@ -869,7 +871,7 @@ __global__ void __launch_bounds__(64) k_solve_grp(NetView nv, GrpView gv, CondVi
     Grp<NSP> x;
     double T;
     grp_setup<NSP, G>(nv, gl, cv, c, kf, kr, ld_k, pj, pfac,
-                      lds + grp_tab_doubles(nv.NRXN, gv.NE, nv.NDYN) +
+                      lds + (TAB ? grp_tab_doubles(nv.NRXN, gv.NE, nv.NDYN) : 0) +
                           (size_t)grp * grp_lds_doubles(nv.NRXN, NSP, nv.NDYN, gv.ND, ga.QB), ga.QB, x, T);
     double y = x.row ? cv.y0[x.gl * cv.ld_y0 + c * cv.s_y0] : 0.0;
     int ns = 0;

@@ -524,6 +524,21 @@ static int grp_shape(const pck_network* net, int nsp, int P, size_t* shm, int* Q
     return PCK_OK;
 }
 
+// LDS copies of the network tables (k_solve_grp<..., TAB = true>) pay when
+// they do not lower the resident waves per CU: min(VGPR-limited waves,
+// LDS-limited blocks) with the tables >= the same without (blocks are one
+// wavefront; 512 VGPRs per lane per SIMD, 160 KiB of LDS per CU on gfx950).
+static bool grp_tables_pay(hipFunction_t f, size_t shm, size_t shm_tab) {
+    int regs = 0;
+    if (hipFuncGetAttribute(&regs, HIP_FUNC_ATTRIBUTE_NUM_REGS, f) != hipSuccess || regs <= 0) return false;
+    const int per_simd = std::min(8, 512 / ((regs + 7) / 8 * 8));
+    const long vgpr_waves = 4L * per_simd;
+    const long lds = 160L * 1024;
+    const long w0 = std::min(vgpr_waves, shm ? lds / (long)shm : vgpr_waves);
+    const long w1 = std::min(vgpr_waves, lds / (long)shm_tab);
+    return w1 >= w0;
+}
+
 static int launch_grp_rates(const pck_network* net, const pck_conditions* cond, const double* kf, const double* kr,
                             int64_t ld_k, const double* y, int64_t ld_y, double* out, int jac, hipStream_t s) {
     if (!net->grp_ok) return fail(PCK_E_SIZE, "lane-group solver: a reaction has more than 6 dynamic participants%s", "");
@@ -662,8 +677,14 @@ static int launch_solve(pck_network* net, const pck_conditions* cond, const pck_
         if (traj && !f) return fail(PCK_E_HIP, "hipRTC compile of the trajectory kernel failed%s", "");
         size_t shm;
         if (f) {
-            rc = grp_shape(net, NS, P, &shm, &ga.QB, true);
+            rc = grp_shape(net, NS, P, &shm, &ga.QB);
             if (rc) return rc;
+            size_t shm_t;
+            int qb_t;
+            if (grp_shape(net, NS, P, &shm_t, &qb_t, true) == PCK_OK && grp_tables_pay(f, shm, shm_t)) {
+                hipFunction_t ft = jit_group_kernel(NS, G, P, traj, true);
+                if (ft) { f = ft; shm = shm_t; }
+            }
             NetView nv = net->nv;
             GrpView gv = net->gv;
             CondView cv = cview(cond);
@@ -673,7 +694,7 @@ static int launch_solve(pck_network* net, const pck_conditions* cond, const pck_
             void* args[] = {&nv, &gv, &cv, &kfp, &krp, &ldk, &a, &ga};
             HIPCHK(hipModuleLaunchKernel(f, g.x, 1, 1, 64, 1, 1, (unsigned)shm, s, args, nullptr));
         } else {
-            rc = grp_shape(net, grp_nsp_ct(NS), grp_p_ct(NS), &shm, &ga.QB, true);
+            rc = grp_shape(net, grp_nsp_ct(NS), grp_p_ct(NS), &shm, &ga.QB);
             if (rc) return rc;
 #define CALL(NP, GG, PP) hipLaunchKernelGGL((k_solve_grp<NP, GG, PP>), g, dim3(64), shm, s, net->nv, net->gv, cview(cond), kf, kr, n, a, ga)
             PCK_GRP_SWITCH(NS, CALL)
