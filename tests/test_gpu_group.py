@@ -458,3 +458,28 @@ def test_ch4_steady_state_solver(P, inputs):
     Y, ok = solver.solve_ode_batch(T=[473.0, 523.0, 573.0])
     assert ok[1] == res.success
     np.testing.assert_allclose(Y[:, 1], res.x, rtol=1e-12, atol=1e-300)
+
+
+@pytest.mark.gpu
+def test_dmtm_patched_rate_model_steady_vs_oracle(P, inputs):
+    """rate_model='patched' (reaction.py:135-162: kads / kdes for non-activated
+    adsorption) through a full device solve: transient to 1e12 s + Newton at
+    three temperatures vs the oracle's scipy BDF + polished root on the same
+    rate constants (1e-6 on coverages above 1e-6)."""
+    s = P.read_from_input_file(os.path.join(inputs, 'DMTM', 'input.json'), rate_model='patched')
+    T = np.array([450.0, 600.0, 750.0])
+    r = s.solve_batch(T=T, tof_terms=('r5', 'r9'), steady=True, rtol=1e-10, atol=1e-14)
+    plan = s.plan(('r5', 'r9'))
+    spec = O.load_spec(os.path.join(inputs, 'DMTM', 'input.json'))
+    for k, t in enumerate(T):
+        m = O.ClassicModel(spec, T=t, mode='patched')
+        yT, _ = m.solve_odes(rtol=1e-10, atol=1e-14)
+        ys = m.find_steady(yT)
+        dyn = [m.idx[nm] for nm in plan.dyn]
+        if not m.regular:
+            assert r['status'][k] in (0, 4), r['status'][k]
+            continue
+        assert r['status'][k] == 0, (t, r['status'][k])
+        big = ys[dyn] > 1e-6
+        np.testing.assert_allclose(r['y'][big, k], ys[dyn][big], rtol=1e-6)
+        np.testing.assert_allclose(r['tof'][k], m.tof(ys, ['r5', 'r9']), rtol=1e-6)
