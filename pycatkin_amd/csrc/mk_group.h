@@ -534,7 +534,7 @@ __device__ __forceinline__ double grp_solve(const Grp<NSP>& x, const LU<NSP>& F,
 template <int NSP, int G, int P, bool TRAJ = false>
 __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& gv, const Grp<NSP>& x, double& y,
                                              double t0, double t_end, double rtol, double atol, int max_steps,
-                                             int& nsteps, bool crows, const TrajOut& to) {
+                                             int& nsteps, bool crows, const TrajOut& to, LU<NSP>& F) {
     using namespace rodas4;
     constexpr bool CLAMP = PCK_GRP_CLAMP && G == 64;    // see put_c
     const int NS = x.NS;
@@ -573,7 +573,6 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
         h = fmin(fmin(100.0 * h0, h1), span);
     }
     double t = t0;
-    LU<NSP> F;
     int blowups = 0;
     int stall = 0;
     int cpv = -1;                                              // conservation law whose pivot row is this lane's
@@ -706,7 +705,7 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
 // Newton steady-state polish (same rules as mk_solver.h: newton)
 template <int NSP, int G, int P>
 __device__ __forceinline__ int grp_newton(const NetView& nv, const GrpView& gv, const Grp<NSP>& x, double& y,
-                                          int iters) {
+                                          int iters, LU<NSP>& F) {
     const int NS = x.NS;
     double b[PCK_MAX_CONS], ci[PCK_MAX_CONS];
     int piv_l[PCK_MAX_CONS];
@@ -722,7 +721,6 @@ __device__ __forceinline__ int grp_newton(const NetView& nv, const GrpView& gv, 
     bool conv = false;
     double prev = INFINITY, lastq = 1.0;
     int linear = 0;
-    LU<NSP> F;
     for (int it = 0; it < iters; ++it) {
         double Gv = grp_rhs<NSP, G>(gv, x, z);
         grp_jac<NSP, G, P>(nv, gv, x, z, 1.0, 0.0, F.W);
@@ -842,8 +840,13 @@ struct GrpArgs {
     int32_t* nsbuf;     // DRC mode: [M][n] integrator steps per perturbation
 };
 
+// occupancy floor of the lane-group solver (waves per SIMD; the VGPR budget
+// follows: 2 -> 256 VGPRs, the NS = 50 kernel then spills in the Newton polish)
+#ifndef PCK_GRP_WAVES
+#define PCK_GRP_WAVES 1
+#endif
 template <int NSP, int G, int P, bool TRAJ = false, bool TAB = false>
-__global__ void __launch_bounds__(64) k_solve_grp(NetView nv, GrpView gv, CondView cv, const double* kf,
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PCK_GRP_WAVES))) k_solve_grp(NetView nv, GrpView gv, CondView cv, const double* kf,
                                                   const double* kr, int64_t ld_k, SolveArgs a, GrpArgs ga) {
     extern __shared__ double lds[];
     const int grp = threadIdx.x / G;
@@ -876,9 +879,10 @@ __global__ void __launch_bounds__(64) k_solve_grp(NetView nv, GrpView gv, CondVi
     double y = x.row ? cv.y0[x.gl * cv.ld_y0 + c * cv.s_y0] : 0.0;
     int ns = 0;
     TrajOut to{a.t_out, a.n_out, a.traj, a.ld_traj, c};
+    LU<NSP> F;                  // one factorisation storage for the transient and the Newton polish
     int st = grp_integrate<NSP, G, P, TRAJ>(nv, gl, x, y, a.t0, a.t_end, a.rtol, a.atol, a.max_steps, ns,
-                                            a.cons_rows != 0, to);
-    if (st == PCK_ST_OK && a.newton) st = grp_newton<NSP, G, P>(nv, gl, x, y, a.newton_iters);
+                                            a.cons_rows != 0, to, F);
+    if (st == PCK_ST_OK && a.newton) st = grp_newton<NSP, G, P>(nv, gl, x, y, a.newton_iters, F);
     const double tof = grp_tof<NSP, G>(nv, gl, x, y);
     const bool fin = gmin<G>((!x.row || isfinite(y)) ? 1.0 : 0.0) > 0.0 && isfinite(tof);
     if (!fin && st == PCK_ST_OK) st = PCK_ST_NONFINITE;

@@ -2,7 +2,7 @@
 conditions of the synthetic config (needs the PCK_TRACE build:
 tools/ab_build.sh trace -DPCK_TRACE; run with PCK_LIB=pycatkin_amd/_ab/lib_trace.so).
 
-    python tools/trace_group.py IDX [IDX ...]      (indices of the 16384-condition synthetic set)
+    python tools/trace_group.py IDX [IDX ...]      (indices of the bench's 65536-condition synthetic set)
 """
 import ctypes as C
 import json
@@ -30,7 +30,7 @@ def main():
                                           rtol=float(sys.argv[3]), atol=float(sys.argv[4])))]
     else:
         sim, _ = synthetic_system()
-        D = np.random.default_rng(0).uniform(-0.5, 0.5, (16384, 4))
+        D = np.random.default_rng(0).uniform(-0.5, 0.5, (65536, 4))     # the bench's synthetic set
         jobs = [(int(a), dict(T=np.full(1, 500.0), desc={'D%d' % k: D[int(a):int(a) + 1, k] for k in range(4)},
                               tof_terms=('R0',), steady=True)) for a in sys.argv[1:]]
     for idx, kw in jobs:
