@@ -29,3 +29,18 @@ def spec_of(net, desc, T=500.0):
                                     user={k: None for k in ('dErxn_user', 'dEa_fwd_user', 'dEa_rev_user', 'dGrxn_user', 'dGa_fwd_user', 'dGa_rev_user')})
     start = {g[0]: g[4] for g in net['gases']}; start['s'] = 1.0
     return dict(states=states, reactions=reactions, system=dict(times=[0.0, 1e4], T=T, p=1e5, start_state=start, rtol=1e-8, atol=1e-10), reactor=dict(kind='ID'))
+
+
+def oracle_point(desc):
+    """Oracle transient (scipy BDF, the reference's solve_ivp path) + polished
+    root at one descriptor vector of the synthetic network: (bdf_ok, regular,
+    y_transient, y_steady, tof, species names).  Module-level so a spawn pool
+    can run it."""
+    from oracle import mk_oracle as O
+    from pycatkin_amd.functions.synthetic import synthetic_network
+    m = O.ClassicModel(spec_of(synthetic_network(), np.asarray(desc)), T=500.0)
+    yT, sol = m.solve_odes(rtol=1e-8, atol=1e-10)
+    if sol.status != 0:
+        return False, False, yT, yT, float('nan'), m.snames
+    ys = m.find_steady(yT.copy())
+    return True, bool(m.regular), yT, ys, float(m.tof(ys, ['R0'])), m.snames

@@ -483,3 +483,49 @@ def test_dmtm_patched_rate_model_steady_vs_oracle(P, inputs):
         big = ys[dyn] > 1e-6
         np.testing.assert_allclose(r['y'][big, k], ys[dyn][big], rtol=1e-6)
         np.testing.assert_allclose(r['tof'][k], m.tof(ys, ['r5', 'r9']), rtol=1e-6)
+
+
+# the one condition of the bench's 65 536 the device still stops on (status 2,
+# the stagnation rule after 99 160 steps) while scipy BDF finishes it
+KNOWN_STALL = {39547}
+
+
+def test_synthetic_former_stragglers_vs_oracle(P, synthetic):
+    """Conditions of the bench's 65 536-condition synthetic set that stalled
+    for up to the 200 000-step budget before the clamped-state transient
+    (17825, 39547) or on which scipy BDF itself stops (37890), plus three
+    ordinary ones, at the library's default step budget.
+    Regular roots of the oracle (scipy BDF + polished root) are matched at
+    1e-6 and degenerate ones end in status 4 with the transient state within
+    1e-3 (floor 1e-9) of scipy's; where scipy BDF itself fails (the reference
+    has no answer) the device still ends with status 0 or 4.  The oracle side
+    runs in a spawn pool (~30 s)."""
+    import multiprocessing as mp
+    from _synth import oracle_point
+    sim, net = synthetic
+    plan = sim.plan(('R0',))
+    D_all = np.random.default_rng(0).uniform(-0.5, 0.5, (65536, 4))
+    idx = [17825, 39547, 37890, 0, 2, 3]
+    D = D_all[idx]
+    r = sim.solve_batch(T=np.full(len(idx), 500.0), desc={'D%d' % k: D[:, k] for k in range(4)},
+                        tof_terms=('R0',), steady=True)
+    with mp.get_context('spawn').Pool(min(len(idx), os.cpu_count() or 1)) as pool:
+        res = pool.map(oracle_point, [d for d in D])
+    checked = 0
+    for j, (bdf_ok, regular, yT, ys, tof, names) in enumerate(res):
+        st = int(r['status'][j])
+        dyn = [names.index(nm) for nm in plan.dyn]
+        if not bdf_ok:                         # the reference path has no answer here
+            assert st in (0, 4), (idx[j], st)
+            continue
+        if idx[j] in KNOWN_STALL:              # parity gap, DESIGN.md "synthetic": reported, not hidden
+            assert st == 2, (idx[j], st)
+            continue
+        assert st == (0 if regular else 4), (idx[j], st, regular)
+        if regular:
+            assert close(r['y'][:, j], ys[dyn], rtol=1e-6, floor=1e-14), (idx[j], np.abs(r['y'][:, j] - ys[dyn]).max())
+            assert abs(r['tof'][j] - tof) <= 1e-6 * abs(tof) + 1e-12, (idx[j], r['tof'][j], tof)
+            checked += 1
+        else:   # degenerate root: two integrators' transients at t_end, bounded by their error
+            assert close(r['y'][:, j], yT[dyn], rtol=1e-3, floor=1e-9), (idx[j], np.abs(r['y'][:, j] - yT[dyn]).max())
+    assert checked >= 2, checked
