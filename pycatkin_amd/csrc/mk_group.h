@@ -194,33 +194,59 @@ __device__ __forceinline__ int ent_species(const uint4& e, int k) {
 }
 
 // net rate of a reaction (record rec) from the group's concentrations
+// Bounds of the record walk: the hipRTC build defines them from the network
+// (most participants of one reaction, largest exponent; csrc/mk_jit.h), the
+// compiled-in kernels use the format's limits.  Unused participant slots of a
+// record are all-zero fields (species 0, exponents 0): they multiply by 1, so
+// the walk runs the fixed bound without a data-dependent loop or branch.
+#ifndef PCK_GRP_NPMAX
+#define PCK_GRP_NPMAX PCK_GRP_MAX_PART
+#endif
+#ifndef PCK_GRP_EMAX
+#define PCK_GRP_EMAX PCK_GRP_MAX_EXP
+#endif
+
+// x^e for 0 <= e <= PCK_GRP_EMAX, branch-free for the usual e <= 2
+__device__ __forceinline__ double spow(double x, int e) {
+    if constexpr (PCK_GRP_EMAX <= 2) {
+        return ((e >= 1) ? x : 1.0) * ((e >= 2) ? x : 1.0);
+    } else {
+        return ipow(x, e);
+    }
+}
+
+// net rate of a reaction (record rec) from the group's concentrations
 __device__ __forceinline__ double rec_rate(const uint4& rec, double a, double b, const double* c) {
-    const int np = rx_np(rec);
-    for (int k = 0; k < np; ++k) {
+    // no FMA contraction: every build (exact-size hipRTC, padded compiled-in)
+    // rounds the products and the difference the same way -- bitwise-equal results
+#pragma clang fp contract(off)
+#pragma unroll
+    for (int k = 0; k < PCK_GRP_NPMAX; ++k) {
         const int f = rx_field(rec, k);
         const double x = c[f & 63];
         const int ef = (f >> 6) & 31, er = f >> 11;
-        if (ef) a *= ipow(x, ef);
-        if (er) b *= ipow(x, er);
+        a *= spow(x, ef);
+        b *= spow(x, er);
     }
     return a - b;
 }
 
 // d(net_r)/d(c_q) for participant k0 of the record's reaction
 __device__ __forceinline__ double rec_drate(const uint4& rec, double kf, double kr, const double* c, int k0) {
-    const int np = rx_np(rec);
+#pragma clang fp contract(off)
     const int f0 = rx_field(rec, k0);
     const int ef0 = (f0 >> 6) & 31, er0 = f0 >> 11;
     const double x0 = c[f0 & 63];
-    double a = ef0 ? kf * (double)ef0 * ipow(x0, ef0 - 1) : 0.0;
-    double b = er0 ? kr * (double)er0 * ipow(x0, er0 - 1) : 0.0;
-    for (int k = 0; k < np; ++k) {
-        if (k == k0) continue;
+    double a = (ef0 > 0) ? kf * (double)ef0 * spow(x0, ef0 - 1) : 0.0;
+    double b = (er0 > 0) ? kr * (double)er0 * spow(x0, er0 - 1) : 0.0;
+#pragma unroll
+    for (int k = 0; k < PCK_GRP_NPMAX; ++k) {
         const int f = rx_field(rec, k);
         const double x = c[f & 63];
-        const int ef = (f >> 6) & 31, er = f >> 11;
-        if (ef) a *= ipow(x, ef);
-        if (er) b *= ipow(x, er);
+        const bool self = (k == k0);
+        const int ef = self ? 0 : (f >> 6) & 31, er = self ? 0 : f >> 11;
+        a *= spow(x, ef);
+        b *= spow(x, er);
     }
     return a - b;
 }
@@ -312,9 +338,12 @@ __device__ __forceinline__ void grp_jac(const NetView& nv, const GrpView& g, con
         const uint4 rec = g.rx[r];
         const int np = rx_np(rec), dp = rx_dptr(rec);
         const double a = x.kf[r], b = x.kr[r];
-        for (int k = 0; k < np; ++k) {
-            const int q = rx_field(rec, k) & 63;
-            x.d[dp + k] = rec_drate(rec, a, b, x.c, k) * nv.dyn[4 * q];     // x cf_q
+#pragma unroll
+        for (int k = 0; k < PCK_GRP_NPMAX; ++k) {
+            if (k < np) {
+                const int q = rx_field(rec, k) & 63;
+                x.d[dp + k] = rec_drate(rec, a, b, x.c, k) * nv.dyn[4 * q];     // x cf_q
+            }
         }
     }
     wsync();
@@ -840,13 +869,18 @@ struct GrpArgs {
     int32_t* nsbuf;     // DRC mode: [M][n] integrator steps per perturbation
 };
 
-// occupancy floor of the lane-group solver (waves per SIMD; the VGPR budget
-// follows: 2 -> 256 VGPRs, the NS = 50 kernel then spills in the Newton polish)
+// occupancy floor of the 64-lane-group solver (waves per SIMD; the VGPR
+// budget follows: 2 -> 256 VGPRs, the NS = 50 kernel then spills in the
+// Newton polish); PCK_GRP_WAVES16 the same for 16/32-lane groups (3 -> 168
+// VGPRs: measured 20 % slower on CH4 than the unconstrained allocation)
 #ifndef PCK_GRP_WAVES
 #define PCK_GRP_WAVES 1
 #endif
+#ifndef PCK_GRP_WAVES16
+#define PCK_GRP_WAVES16 1
+#endif
 template <int NSP, int G, int P, bool TRAJ = false, bool TAB = false>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PCK_GRP_WAVES))) k_solve_grp(NetView nv, GrpView gv, CondView cv, const double* kf,
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 64 ? PCK_GRP_WAVES : PCK_GRP_WAVES16))) k_solve_grp(NetView nv, GrpView gv, CondView cv, const double* kf,
                                                   const double* kr, int64_t ld_k, SolveArgs a, GrpArgs ga) {
     extern __shared__ double lds[];
     const int grp = threadIdx.x / G;

@@ -29,6 +29,7 @@ struct pck_network {
     double* d_dp = nullptr;
     void* d_grp = nullptr;          // lane-group plan (mk_group.h): reaction records, species CSR of S
     int grp_ok = 0;                 // every reaction fits a record (<= 6 participants, exponents <= 31)
+    int grp_npmax = 0, grp_emax = 0;  // most participants of a reaction / largest exponent (hipRTC bounds)
     GrpView gv;
     int spec = 0;                   // id of the compiled-in plan (networks.h) or 0
     int plan_mode = PCK_PLAN_AUTO;  // pck_network_set_plan_mode
@@ -270,12 +271,14 @@ extern "C" int pck_network_create(const int32_t* ip, int64_t n_ip, const double*
                     net->grp_ok = 0;
                     continue;
                 }
+                net->grp_emax = std::max(net->grp_emax, std::max(ea, eb));
                 const uint32_t f = (uint32_t)i | ((uint32_t)ea << 6) | ((uint32_t)eb << 11);
                 w[n >> 1] |= f << (16 * (n & 1));
                 spv[6 * j + n] = i;
                 ++n;
             }
             npv[j] = n;
+            net->grp_npmax = std::max(net->grp_npmax, n);
             dpv[j] = ND;
             ND += n;
             rx[4 * j + 0] = w[0]; rx[4 * j + 1] = w[1]; rx[4 * j + 2] = w[2];
@@ -673,7 +676,7 @@ static int launch_solve(pck_network* net, const pck_conditions* cond, const pck_
         dim3 g((unsigned)((groups + per - 1) / per));
         hipFunction_t f = nullptr;
         int P = grp_p(NS);
-        if ((net->plan_mode != PCK_PLAN_RUNTIME || traj) && jit_enabled()) f = jit_group_kernel(NS, G, P, traj);
+        if ((net->plan_mode != PCK_PLAN_RUNTIME || traj) && jit_enabled()) f = jit_group_kernel(NS, G, P, traj, false, net->grp_npmax, net->grp_emax);
         if (traj && !f) return fail(PCK_E_HIP, "hipRTC compile of the trajectory kernel failed%s", "");
         size_t shm;
         if (f) {
@@ -682,7 +685,7 @@ static int launch_solve(pck_network* net, const pck_conditions* cond, const pck_
             size_t shm_t;
             int qb_t;
             if (grp_shape(net, NS, P, &shm_t, &qb_t, true) == PCK_OK && grp_tables_pay(f, shm, shm_t)) {
-                hipFunction_t ft = jit_group_kernel(NS, G, P, traj, true);
+                hipFunction_t ft = jit_group_kernel(NS, G, P, traj, true, net->grp_npmax, net->grp_emax);
                 if (ft) { f = ft; shm = shm_t; }
             }
             NetView nv = net->nv;
