@@ -205,6 +205,9 @@ __device__ __forceinline__ int ent_species(const uint4& e, int k) {
 #ifndef PCK_GRP_EMAX
 #define PCK_GRP_EMAX PCK_GRP_MAX_EXP
 #endif
+#ifndef PCK_GRP_DEGMAX
+#define PCK_GRP_DEGMAX 0        // largest row degree of the species CSR (0: data-dependent row loops)
+#endif
 
 // x^e for 0 <= e <= PCK_GRP_EMAX, branch-free for the usual e <= 2
 __device__ __forceinline__ double spow(double x, int e) {
@@ -309,8 +312,24 @@ __device__ __forceinline__ double grp_rhs(const GrpView& g, const Grp<NSP>& x, d
     wsync();
     double f = 0.0;
     if (x.row) {
-        // two partial sums and a 4-deep unroll keep several entry loads in flight
+        // two partial sums keep several entry loads in flight
         double f2 = 0.0;
+#if PCK_GRP_DEGMAX > 0
+        // hipRTC build: the trip count is the network's largest row degree,
+        // the same for every lane (scalar loop control)
+#pragma unroll 2
+        for (int i = 0; i < PCK_GRP_DEGMAX; i += 2) {
+            const int e = x.rb + i;
+            if (e + 1 < x.re) {                 // lanes past their row's end are masked: no LDS traffic
+                const uint4 q = g.ent[e], q2 = g.ent[e + 1];
+                f = fma(ent_s(q), x.d[ent_r(q)], f);
+                f2 = fma(ent_s(q2), x.d[ent_r(q2)], f2);
+            } else if (e < x.re) {
+                const uint4 q = g.ent[e];
+                f = fma(ent_s(q), x.d[ent_r(q)], f);
+            }
+        }
+#else
         int e = x.rb;
 #pragma unroll 2
         for (; e + 1 < x.re; e += 2) {
@@ -322,6 +341,7 @@ __device__ __forceinline__ double grp_rhs(const GrpView& g, const Grp<NSP>& x, d
             const uint4 q = g.ent[e];
             f = fma(ent_s(q), x.d[ent_r(q)], f);
         }
+#endif
         f = (f + f2) * x.rs + x.fl * (x.in - y);
     }
     return f;
@@ -354,6 +374,21 @@ __device__ __forceinline__ void grp_jac(const NetView& nv, const GrpView& g, con
         const int q0 = pass * QB;
         if (x.row) {
             double* jr = x.J + x.gl * QB - q0;
+#if PCK_GRP_DEGMAX > 0
+#pragma unroll 2
+            for (int i = 0; i < PCK_GRP_DEGMAX; ++i) {
+                if (x.rb + i >= x.re) continue;      // masked lanes: no LDS traffic
+                const uint4 q = g.ent[x.rb + i];
+                const double s = ent_s(q);
+                const int np = ent_np(q), dp = ent_dptr(q);
+#pragma unroll
+                for (int k = 0; k < PCK_GRP_NPMAX; ++k) {
+                    const int sp = ent_species(q, k);
+                    // only the owner lane adds to its row: program order = summation order
+                    if (k < np && (P == 1 || (sp >= q0 && sp < q0 + QB))) atomicAdd(jr + sp, s * x.d[dp + k]);
+                }
+            }
+#else
 #pragma unroll 4
             for (int e = x.rb; e < x.re; ++e) {
                 const uint4 q = g.ent[e];
@@ -365,6 +400,7 @@ __device__ __forceinline__ void grp_jac(const NetView& nv, const GrpView& g, con
                     if (P == 1 || (sp >= q0 && sp < q0 + QB)) atomicAdd(jr + sp, s * x.d[dp + k]);
                 }
             }
+#endif
         }
         wsync();
 #pragma unroll
