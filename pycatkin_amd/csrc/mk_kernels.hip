@@ -689,7 +689,8 @@ static int launch_solve(pck_network* net, const pck_conditions* cond, const pck_
             f = jit_group_kernel(NS, G, P, traj, false, net->grp_npmax, net->grp_emax, 0);
             // uniform row loops bounded by the largest row degree (PCK_GRP_DEGMAX):
             // an A/B option (PCK_GRP_DEGMAX=1), taken only where they keep the
-            // occupancy; measured with unmasked slots DMTM DRC +5 %, CH4 -13 %
+            // occupancy; measured slower (CH4 100.6 k -> 83.6 k solves/s, DMTM
+            // DRC 68.5 k -> 67.3 k; profiles/r2/configs/ab_degmax.txt)
             const char* ev = getenv("PCK_GRP_DEGMAX");
             hipFunction_t fd = (f && ev && ev[0] == '1')
                                    ? jit_group_kernel(NS, G, P, traj, false, net->grp_npmax, net->grp_emax,
