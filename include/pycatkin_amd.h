@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define PCK_ABI_VERSION 2
+#define PCK_ABI_VERSION 3
 
 /* error codes */
 #define PCK_OK 0
@@ -143,6 +143,12 @@ typedef struct {
     double drc_eps;        /* pck_drc only: relative k perturbation */
     const double* t_out;   /* pck_solve: n_out ascending sample times in [t0, t_end] (device), or NULL */
     int64_t n_out;         /*   the state at each is written to pck_outputs.traj (dense output) */
+    double retry_rtol;     /* with newton: a condition whose polish meets a degenerate root */
+    double retry_atol;     /*   (PCK_ST_NEWTON) is integrated again, t0..t_end, at these tolerances,
+                            *   in the same launch (0: off); its y / tof become that transient end,
+                            *   the reference's System.activity semantics (old_system.py:517-529),
+                            *   status stays PCK_ST_NEWTON (or the retry's failure status) and
+                            *   nsteps adds the retry's steps */
 } pck_solve_params;
 
 /* Outputs of pck_solve (device pointers; any may be NULL). */

@@ -611,7 +611,13 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
     const double invNS = 1.0 / NS;
     nsteps = 0;
     const double span = t_end - t0;
-    if (!(span > 0.0)) return PCK_ST_OK;
+    if (!(span > 0.0)) {
+        if constexpr (TRAJ) {
+            for (; ko < to.n; ++ko)
+                if (x.row) to.y[((int64_t)ko * NS + x.gl) * to.ld + to.c] = y;
+        }
+        return PCK_ST_OK;
+    }
     double F0 = grp_rhs<NSP, G, CLAMP>(gv, x, y);
     double cons0[PCK_MAX_CONS];
     double ci[PCK_MAX_CONS];
@@ -763,6 +769,10 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
         if (stall > PCK_STALL_STEPS) return PCK_ST_STEPFAIL;
         // scipy's BDF limit: a step below 10 ulp(t) is a failure
         if (!(h > 2.220446049250313e-15 * fmax(fabs(t), 1e-300)) && t < t_end) return PCK_ST_STEPFAIL;
+    }
+    if constexpr (TRAJ) {                       // samples past t_end (rounding of the caller's grid)
+        for (; ko < to.n; ++ko)
+            if (x.row) to.y[((int64_t)ko * NS + x.gl) * to.ld + to.c] = y;
     }
     return PCK_ST_OK;
 }
@@ -921,7 +931,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 64
     extern __shared__ double lds[];
     const int grp = threadIdx.x / G;
     const int64_t v = (int64_t)blockIdx.x * (64 / G) + grp;
-    const int64_t c = v / ga.M;
+    const int64_t slot = v / ga.M;
     const int q = (int)(v % ga.M);
     const int R1 = nv.NRXN > 0 ? nv.NRXN : 1, NE1 = gv.NE > 0 ? gv.NE : 1;
     GrpView gl = gv;                                // TAB: the tables, copied to LDS by the whole block (one wave)
@@ -937,7 +947,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 64
         gl.ent = tent;
         gl.row = trow;
     }
-    if (c >= cv.n) return;                          // group-uniform exit; no block barriers below
+    if (slot >= cv.n) return;                       // group-uniform exit; no block barriers below
+    const int64_t c = slot;
     int pj = -1;
     double pfac = 1.0;
     if (q > 0) { pj = (q - 1) >> 1; pfac = (q & 1) ? 1.0 + a.eps : 1.0 - a.eps; }
@@ -946,13 +957,29 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 64
     grp_setup<NSP, G>(nv, gl, cv, c, kf, kr, ld_k, pj, pfac,
                       lds + (TAB ? grp_tab_doubles(nv.NRXN, gv.NE, nv.NDYN) : 0) +
                           (size_t)grp * grp_lds_doubles(nv.NRXN, NSP, nv.NDYN, gv.ND, ga.QB), ga.QB, x, T);
-    double y = x.row ? cv.y0[x.gl * cv.ld_y0 + c * cv.s_y0] : 0.0;
+    double y = 0.0;
     int ns = 0;
     TrajOut to{a.t_out, a.n_out, a.traj, a.ld_traj, c};
     LU<NSP> F;                  // one factorisation storage for the transient and the Newton polish
-    int st = grp_integrate<NSP, G, P, TRAJ>(nv, gl, x, y, a.t0, a.t_end, a.rtol, a.atol, a.max_steps, ns,
+    // transient, polish and -- for a degenerate root -- the retry transient at
+    // a.retry_rtol / retry_atol (mk_solver.h: solve_lane; group-uniform)
+    int st = PCK_ST_OK;
+    double rtol = a.rtol, atol = a.atol;
+    for (int pass = 0; pass < 2; ++pass) {
+        y = x.row ? cv.y0[x.gl * cv.ld_y0 + c * cv.s_y0] : 0.0;
+        int nsp = 0;
+        st = grp_integrate<NSP, G, P, TRAJ>(nv, gl, x, y, a.t0, a.t_end, rtol, atol, a.max_steps, nsp,
                                             a.cons_rows != 0, to, F);
-    if (st == PCK_ST_OK && a.newton) st = grp_newton<NSP, G, P>(nv, gl, x, y, a.newton_iters, F);
+        ns += nsp;
+        if (pass == 1) {
+            if (st == PCK_ST_OK) st = PCK_ST_NEWTON;
+            break;
+        }
+        if (st == PCK_ST_OK && a.newton) st = grp_newton<NSP, G, P>(nv, gl, x, y, a.newton_iters, F);
+        if (!(st == PCK_ST_NEWTON && a.retry_rtol > 0.0)) break;
+        rtol = a.retry_rtol;
+        atol = a.retry_atol;
+    }
     const double tof = grp_tof<NSP, G>(nv, gl, x, y);
     const bool fin = gmin<G>((!x.row || isfinite(y)) ? 1.0 : 0.0) > 0.0 && isfinite(tof);
     if (!fin && st == PCK_ST_OK) st = PCK_ST_NONFINITE;

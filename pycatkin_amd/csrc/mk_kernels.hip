@@ -14,6 +14,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <atomic>
 #include <mutex>
 #include <new>
 #include <vector>
@@ -36,8 +37,10 @@ struct pck_network {
     int plan_mode = PCK_PLAN_AUTO;  // pck_network_set_plan_mode
     unsigned long long digest = 0;
     std::string jit_src;            // mk_jit.h: constexpr plan source for hipRTC (lane networks without a compiled plan)
-    bool jit_on = false;            // the last lane solve ran the hipRTC-compiled plan
-    bool grp_jit_on = false;        // the last lane-group solve ran the exact-size hipRTC kernel
+    // diagnostics of the last solve (pck_network_dims), the only fields a solve
+    // writes: atomic, so calls from several host threads stay race-free
+    mutable std::atomic<bool> jit_on{false};      // the last lane solve ran the hipRTC-compiled plan
+    mutable std::atomic<bool> grp_jit_on{false};  // the last lane-group solve ran the exact-size hipRTC kernel
 };
 
 // FNV-1a 64 over the solver-side structure (network.py: structural_digest)
@@ -361,7 +364,7 @@ extern "C" int pck_network_dims(const pck_network* net, int32_t* dims) {
     const NetView& v = net->nv;
     dims[0] = v.D; dims[1] = v.NTH; dims[2] = v.NREG; dims[3] = v.NRXN; dims[4] = v.NDYN;
     dims[5] = v.NFIX; dims[6] = v.NCONS; dims[7] = v.NTOF; dims[8] = v.nfeat;
-    dims[9] = net->spec ? net->spec : net->jit_on ? PCK_SPEC_JIT : 0;
+    dims[9] = net->spec ? net->spec : net->jit_on.load(std::memory_order_relaxed) ? PCK_SPEC_JIT : 0;
     return PCK_OK;
 }
 
@@ -625,58 +628,18 @@ static int check_params(const pck_solve_params* prm) {
     if (!(prm->rtol > 0.0) || !(prm->atol > 0.0)) return fail(PCK_E_ARG, "tolerances must be positive%s", "");
     if (prm->max_steps < 1) return fail(PCK_E_ARG, "max_steps must be >= 1%s", "");
     if (prm->newton && (prm->newton_iters < 1 || prm->newton_iters > 200)) return fail(PCK_E_ARG, "newton_iters%s out of range", "");
+    if (prm->retry_rtol != 0.0 && !(prm->retry_rtol > 0.0 && prm->retry_atol > 0.0))
+        return fail(PCK_E_ARG, "retry tolerances must both be positive (or retry_rtol 0)%s", "");
     return PCK_OK;
 }
 
-// kf / kr of the batch go to `kscr` (per-call, stream-ordered): [2][R][n]
-static int launch_solve(pck_network* net, const pck_conditions* cond, const pck_solve_params* prm, SolveArgs a,
-                        hipStream_t s, StreamScratch& kscr, int drc_groups = 0) {
+// One solver launch over the batch (lane or lane-group path).
+static int run_solver(const pck_network* net, const pck_conditions* cond, const SolveArgs& a_in, bool grp,
+                      GrpArgs& ga, bool traj, const double* kf, const double* kr, hipStream_t s) {
+    SolveArgs a = a_in;
     const int64_t n = cond->n;
-    if (n == 0) return PCK_OK;
-    if (!cond->y0) return fail(PCK_E_ARG, "initial state y0 required%s", "");
-    const int R = net->nv.NRXN;
-    int rc = salloc(kscr, sizeof(double) * 2 * (size_t)(R > 0 ? R : 1) * n, s);
-    if (rc) return rc;
-    double* kf = kscr.as<double>();
-    double* kr = kf + (int64_t)(R > 0 ? R : 1) * n;
-    rc = launch_rate_constants(net, cond, kf, kr, n, s);
-    if (rc) return rc;
-    a.t0 = prm->t0; a.t_end = prm->t_end; a.rtol = prm->rtol; a.atol = prm->atol; a.eps = prm->drc_eps;
-    a.max_steps = prm->max_steps; a.newton = prm->newton; a.newton_iters = prm->newton_iters;
-    a.want_activity = prm->want_activity;
-    const bool traj = (prm->n_out > 0 && a.traj != nullptr);
-    if (traj) {
-        if (!prm->t_out) return fail(PCK_E_ARG, "n_out > 0 without t_out%s", "");
-        if (drc_groups || a.G != 1) return fail(PCK_E_ARG, "trajectory output is for pck_solve only%s", "");
-        if (!jit_enabled()) return fail(PCK_E_ARG, "trajectory output needs the hipRTC kernels (PCK_JIT=0 is set)%s", "");
-        a.t_out = prm->t_out;
-        a.n_out = (int)prm->n_out;
-    }
-    {
-        // conservation rows in the stage systems (mk_solver.h: cons_rows) are
-        // off by default: measured on examples/DMTM at 400 K they cost 1.5x
-        // (GPU) to 2.6x (numpy restatement) more steps -- the pivot species
-        // inherits the cancellation of the other coverages' increments
-        const char* e = getenv("PCK_CONS_ROWS");
-        a.cons_rows = (e && e[0] == '1');
-    }
-    if (drc_groups || use_group(net, a.G)) {
-        if (!net->grp_ok)
-            return fail(PCK_E_SIZE, "lane-group solver: a reaction has more than 6 dynamic participants%s", "");
-        GrpArgs ga;
-        ga.M = drc_groups ? drc_groups : 1;
-        ga.tofbuf = nullptr;
-        ga.stbuf = nullptr;
-        ga.nsbuf = nullptr;
-        StreamScratch dscr;
-        if (drc_groups) {
-            const int64_t m = (int64_t)drc_groups * n;
-            rc = salloc(dscr, sizeof(double) * m + 2 * sizeof(int32_t) * m, s);
-            if (rc) return rc;
-            ga.tofbuf = dscr.as<double>();
-            ga.stbuf = (int32_t*)(ga.tofbuf + m);
-            ga.nsbuf = ga.stbuf + m;
-        }
+    int rc;
+    if (grp) {
         const int NS = net->nv.NDYN;
         const int G = grp_g(NS);
         const int per = 64 / G;
@@ -724,16 +687,12 @@ static int launch_solve(pck_network* net, const pck_conditions* cond, const pck_
             PCK_GRP_SWITCH(NS, CALL)
 #undef CALL
         }
-        net->grp_jit_on = (f != nullptr);
+        net->grp_jit_on.store(f != nullptr, std::memory_order_relaxed);
         HIPCHK(hipGetLastError());
-        if (drc_groups) {
-            hipLaunchKernelGGL(k_drc_combine, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, R, a.eps,
-                               ga.tofbuf, ga.stbuf, ga.nsbuf, a.xi, a.ld_xi, a.tof0, a.status, a.nsteps);
-            HIPCHK(hipGetLastError());
-        }
         return PCK_OK;
     }
     const int B = PCK_SOLVE_BLOCK;
+    const int R = net->nv.NRXN;
     const int64_t lanes = n * a.G;
     const size_t shm = lds_bytes(R, net->nv.NDYN, B);
     dim3 g((unsigned)((lanes + B - 1) / B));
@@ -757,7 +716,7 @@ static int launch_solve(pck_network* net, const pck_conditions* cond, const pck_
         hipFunction_t f = nullptr;
         if (net->plan_mode == PCK_PLAN_AUTO && !net->jit_src.empty() && jit_enabled())
             f = jit_kernel(net->digest, net->jit_src);
-        net->jit_on = (f != nullptr);
+        net->jit_on.store(f != nullptr, std::memory_order_relaxed);
         if (f) {
             NetView nv = net->nv;
             CondView cv = cview(cond);
@@ -773,6 +732,69 @@ static int launch_solve(pck_network* net, const pck_conditions* cond, const pck_
         }
     }
     HIPCHK(hipGetLastError());
+    return PCK_OK;
+}
+
+// kf / kr of the batch go to `kscr` (per-call, stream-ordered): [2][R][n]
+static int launch_solve(const pck_network* net, const pck_conditions* cond, const pck_solve_params* prm, SolveArgs a,
+                        hipStream_t s, StreamScratch& kscr, int drc_groups = 0) {
+    const int64_t n = cond->n;
+    if (n == 0) return PCK_OK;
+    if (!cond->y0) return fail(PCK_E_ARG, "initial state y0 required%s", "");
+    const int R = net->nv.NRXN;
+    int rc = salloc(kscr, sizeof(double) * 2 * (size_t)(R > 0 ? R : 1) * n, s);
+    if (rc) return rc;
+    double* kf = kscr.as<double>();
+    double* kr = kf + (int64_t)(R > 0 ? R : 1) * n;
+    rc = launch_rate_constants(net, cond, kf, kr, n, s);
+    if (rc) return rc;
+    a.t0 = prm->t0; a.t_end = prm->t_end; a.rtol = prm->rtol; a.atol = prm->atol; a.eps = prm->drc_eps;
+    a.max_steps = prm->max_steps; a.newton = prm->newton; a.newton_iters = prm->newton_iters;
+    a.want_activity = prm->want_activity;
+    // degenerate roots (status 4) re-integrated in the same launch (mk_solver.h: solve_lane)
+    a.retry_rtol = prm->newton ? prm->retry_rtol : 0.0;
+    a.retry_atol = prm->retry_atol;
+    const bool traj = (prm->n_out > 0 && a.traj != nullptr);
+    if (traj) {
+        if (!prm->t_out) return fail(PCK_E_ARG, "n_out > 0 without t_out%s", "");
+        if (drc_groups || a.G != 1) return fail(PCK_E_ARG, "trajectory output is for pck_solve only%s", "");
+        if (!jit_enabled()) return fail(PCK_E_ARG, "trajectory output needs the hipRTC kernels (PCK_JIT=0 is set)%s", "");
+        a.t_out = prm->t_out;
+        a.n_out = (int)prm->n_out;
+    }
+    {
+        // conservation rows in the stage systems (mk_solver.h: cons_rows) are
+        // off by default: measured on examples/DMTM at 400 K they cost 1.5x
+        // (GPU) to 2.6x (numpy restatement) more steps -- the pivot species
+        // inherits the cancellation of the other coverages' increments
+        const char* e = getenv("PCK_CONS_ROWS");
+        a.cons_rows = (e && e[0] == '1');
+    }
+    const bool grp = drc_groups || use_group(net, a.G);
+    if (grp && !net->grp_ok)
+        return fail(PCK_E_SIZE, "lane-group solver: a reaction has more than 6 dynamic participants%s", "");
+    GrpArgs ga;
+    ga.M = drc_groups ? drc_groups : 1;
+    ga.QB = 1;
+    ga.tofbuf = nullptr;
+    ga.stbuf = nullptr;
+    ga.nsbuf = nullptr;
+    StreamScratch dscr;
+    if (drc_groups) {
+        const int64_t m = (int64_t)drc_groups * n;
+        rc = salloc(dscr, sizeof(double) * m + 2 * sizeof(int32_t) * m, s);
+        if (rc) return rc;
+        ga.tofbuf = dscr.as<double>();
+        ga.stbuf = (int32_t*)(ga.tofbuf + m);
+        ga.nsbuf = ga.stbuf + m;
+    }
+    rc = run_solver(net, cond, a, grp, ga, traj, kf, kr, s);
+    if (rc) return rc;
+    if (drc_groups) {
+        hipLaunchKernelGGL(k_drc_combine, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, R, a.eps,
+                           ga.tofbuf, ga.stbuf, ga.nsbuf, a.xi, a.ld_xi, a.tof0, a.status, a.nsteps);
+        HIPCHK(hipGetLastError());
+    }
     return PCK_OK;
 }
 
@@ -795,10 +817,8 @@ extern "C" int pck_solve(const pck_network* net, const pck_conditions* cond, con
     }
     if ((out->kf || out->kr) && cond->n > 0 && (out->ld_k < cond->n || !out->kf || !out->kr))
         return fail(PCK_E_ARG, "kf/kr dump needs both arrays%s", "");
-    // the network is not modified; const_cast only for the hipRTC bookkeeping flag
-    pck_network* nn = const_cast<pck_network*>(net);
     StreamScratch kscr;
-    rc = launch_solve(nn, cond, prm, a, (hipStream_t)stream, kscr);
+    rc = launch_solve(net, cond, prm, a, (hipStream_t)stream, kscr);
     if (rc) return rc;
     if ((out->kf || out->kr) && cond->n > 0) {
         const int R = net->nv.NRXN;
@@ -826,9 +846,8 @@ extern "C" int pck_drc(const pck_network* net, const pck_conditions* cond, const
     SolveArgs a;
     memset(&a, 0, sizeof(a));
     a.xi = xi; a.ld_xi = ld_xi; a.tof0 = tof0; a.status = status; a.nsteps = nsteps; a.G = G;
-    pck_network* nn = const_cast<pck_network*>(net);
     StreamScratch kscr;
     // lane-group networks: one group per (condition, perturbation), combined after
-    if (use_group(net, G)) return launch_solve(nn, cond, prm, a, (hipStream_t)stream, kscr, 2 * R + 1);
-    return launch_solve(nn, cond, prm, a, (hipStream_t)stream, kscr);
+    if (use_group(net, G)) return launch_solve(net, cond, prm, a, (hipStream_t)stream, kscr, 2 * R + 1);
+    return launch_solve(net, cond, prm, a, (hipStream_t)stream, kscr);
 }

@@ -285,6 +285,11 @@ __device__ __forceinline__ void cons_zero(const P& p, double (&b)[NS]) {
 #ifndef PCK_CONS_ROWS
 #define PCK_CONS_ROWS 0
 #endif
+// integrate / newton are inlined into the kernel (see DESIGN.md "Runtime-plan
+// fault"); -DPCK_LANE_INLINE=__noinline__ builds the call variant for study
+#ifndef PCK_LANE_INLINE
+#define PCK_LANE_INLINE __forceinline__
+#endif
 
 namespace rodas4 {
 constexpr double g = 0.25;
@@ -326,7 +331,7 @@ struct TrajOut {
 };
 
 template <bool TRAJ, class P, class K>
-__device__ __forceinline__ int integrate(const P& p, const Lane<P::NS>& L, const K& k, double (&y)[P::NS], double t0,
+__device__ PCK_LANE_INLINE int integrate(const P& p, const Lane<P::NS>& L, const K& k, double (&y)[P::NS], double t0,
                          double t_end, double rtol, double atol, int max_steps, int& nsteps, bool crows,
                          const TrajOut& to) {
     using namespace rodas4;
@@ -340,7 +345,15 @@ __device__ __forceinline__ int integrate(const P& p, const Lane<P::NS>& L, const
     }
     nsteps = 0;
     const double span = t_end - t0;
-    if (!(span > 0.0)) return PCK_ST_OK;
+    if (!(span > 0.0)) {
+        if constexpr (TRAJ) {
+            for (; ko < to.n; ++ko) {
+#pragma unroll
+                for (int i = 0; i < NS; ++i) to.y[((int64_t)ko * NS + i) * to.ld + to.c] = y[i];
+            }
+        }
+        return PCK_ST_OK;
+    }
     double F0[NS];
     rhs(p, L, k, y, F0);
     double cons0[PCK_MAX_CONS];
@@ -553,6 +566,14 @@ __device__ __forceinline__ int integrate(const P& p, const Lane<P::NS>& L, const
         // scipy's BDF limit: a step below 10 ulp(t) is a failure
         if (!(h > 2.220446049250313e-15 * fmax(fabs(t), 1e-300)) && t < t_end) return PCK_ST_STEPFAIL;
     }
+    if constexpr (TRAJ) {
+        // samples past t_end (a caller's log grid can round one ulp above it)
+        // take the final state
+        for (; ko < to.n; ++ko) {
+#pragma unroll
+            for (int i = 0; i < NS; ++i) to.y[((int64_t)ko * NS + i) * to.ld + to.c] = y[i];
+        }
+    }
     return PCK_ST_OK;
 }
 
@@ -563,7 +584,7 @@ __device__ __forceinline__ int integrate(const P& p, const Lane<P::NS>& L, const
 // convergent (a site-starved surface approached algebraically) or lands on a
 // negative component is not regular -> PCK_ST_NEWTON, transient state kept.
 template <class P, class K>
-__device__ __forceinline__ int newton(const P& p, const Lane<P::NS>& L, const K& k, double (&y)[P::NS], int iters) {
+__device__ PCK_LANE_INLINE int newton(const P& p, const Lane<P::NS>& L, const K& k, double (&y)[P::NS], int iters) {
     constexpr int NS = P::NS;
     double b[PCK_MAX_CONS];
     for (int l = 0; l < p.ncons(); ++l) {
@@ -730,7 +751,39 @@ struct SolveArgs {
     int cons_rows;                             // conservation rows in the stage systems (A/B: PCK_CONS_ROWS=1)
     const double* t_out; int n_out;            // trajectory sample times (k_solve<P, true>)
     double* traj; int64_t ld_traj;             // [n_out][NS][ld_traj]
+    // degenerate-root retry (pck_solve_params.retry_rtol; 0 = off): a lane
+    // whose polish ends in PCK_ST_NEWTON integrates again from y0 at these
+    // tolerances, in the same launch, and reports that transient end
+    double retry_rtol, retry_atol;
 };
+
+// One condition's solve: transient, optional Newton polish and, for a
+// degenerate root, the retry transient (the pass loop keeps one inlined copy
+// of the integrator).  The lanes of a wave run pass 0 together; the lanes that
+// retry start pass 1 together, so the integrator's wave-uniform step counter
+// stays uniform.  Returns the status; ns = steps of both passes.
+template <bool TRAJ, class P, class K>
+__device__ __forceinline__ int solve_lane(const P& p, const Lane<P::NS>& L, const K& k, const CondView& cv,
+                                          int64_t c, const SolveArgs& a, double (&y)[P::NS], int& ns,
+                                          const TrajOut& to) {
+    constexpr int NS = P::NS;
+    double rtol = a.rtol, atol = a.atol;
+    int st = PCK_ST_OK;
+    ns = 0;
+    for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+        for (int i = 0; i < NS; ++i) y[i] = cv.y0[i * cv.ld_y0 + c * cv.s_y0];
+        int nsp = 0;
+        st = integrate<TRAJ>(p, L, k, y, a.t0, a.t_end, rtol, atol, a.max_steps, nsp, a.cons_rows != 0, to);
+        ns += nsp;
+        if (pass == 1) return (st == PCK_ST_OK) ? PCK_ST_NEWTON : st;
+        if (st == PCK_ST_OK && a.newton) st = newton(p, L, k, y, a.newton_iters);
+        if (!(st == PCK_ST_NEWTON && a.retry_rtol > 0.0)) break;
+        rtol = a.retry_rtol;
+        atol = a.retry_atol;
+    }
+    return st;
+}
 
 template <class P>
 struct KFor {
@@ -785,11 +838,8 @@ __global__ void __launch_bounds__(PCK_SOLVE_BLOCK) __attribute__((amdgpu_waves_p
         T = L.T;
         load_keff(p, nv, cv, c, kf, kr, ld_k, k, pj, pfac);
         double y[NS];
-#pragma unroll
-        for (int i = 0; i < NS; ++i) y[i] = cv.y0[i * cv.ld_y0 + c * cv.s_y0];
         TrajOut to{a.t_out, a.n_out, a.traj, a.ld_traj, c};
-        st = integrate<TRAJ>(p, L, k, y, a.t0, a.t_end, a.rtol, a.atol, a.max_steps, ns, a.cons_rows != 0, to);
-        if (st == PCK_ST_OK && a.newton) st = newton(p, L, k, y, a.newton_iters);
+        st = solve_lane<TRAJ>(p, L, k, cv, c, a, y, ns, to);
         tof = lane_tof(p, nv, k, y);
         bool fin = isfinite(tof);
 #pragma unroll

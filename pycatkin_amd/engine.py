@@ -170,11 +170,16 @@ class DeviceNetwork:
 
     @staticmethod
     def params(t_end, t0=0.0, rtol=1e-8, atol=1e-10, max_steps=100000, newton=False, newton_iters=30,
-               activity=False, drc_eps=1e-3):
+               activity=False, drc_eps=1e-3, retry=None):
+        """retry = (rtol, atol): with newton, the conditions whose polish meets a
+        degenerate root (status 4) are integrated again at these tolerances
+        and report that transient end (pck_solve_params.retry_rtol)."""
         p = L.SolveParams()
         p.t0, p.t_end, p.rtol, p.atol = float(t0), float(t_end), float(rtol), float(atol)
         p.max_steps, p.newton, p.newton_iters = int(max_steps), int(bool(newton)), int(newton_iters)
         p.want_activity, p.drc_eps = int(bool(activity)), float(drc_eps)
+        if retry is not None:
+            p.retry_rtol, p.retry_atol = float(retry[0]), float(retry[1])
         return p
 
     def solve(self, n, T, p, y0, desc=None, fixc=None, inflow=None, want_k=False, out=None, t_out=None, **kw):
@@ -203,7 +208,8 @@ class DeviceNetwork:
         if 'kf' in out:
             o.kf, o.kr, o.ld_k = _ptr(out['kf']), _ptr(out['kr']), n
         if tt is not None and tt.numel():
-            out['traj'] = torch.empty((tt.numel(), self.NDYN, n), dtype=torch.float64, device='cuda')
+            # samples a failed solve never reaches stay NaN
+            out['traj'] = torch.full((tt.numel(), self.NDYN, n), float('nan'), dtype=torch.float64, device='cuda')
             o.traj, o.ld_traj = _ptr(out['traj']), n
         L.check(self.lib.pck_solve(self.h, C.byref(c), C.byref(prm), C.byref(o), _stream(torch)))
         return out

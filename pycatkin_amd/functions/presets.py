@@ -185,3 +185,125 @@ def _save(sim_system, plan, label, stem, xs, final, rates, drcs, tof_terms, csv_
         vals = np.array([[x] + [drcs[x][r] for r in sim_system.reactions] for x in xs])
         pd.DataFrame(vals, columns=[label] + list(sim_system.reactions)).to_csv(
             csv_path + 'drcs_vs_%s.csv' % suffix, index=False)
+
+
+# ----------------------------------------------------------------------------
+# energy tables (presets.py:378-472), every number from one pck_energies launch
+# ----------------------------------------------------------------------------
+def _mkdir(csv_path):
+    if csv_path and not os.path.isdir(csv_path):
+        os.makedirs(csv_path, exist_ok=True)
+
+
+def _reaction_energy_rows(sim_system, T, p):
+    """[dEr, dGr, dEa, dGa] (J/mol) of every reaction at (T, p): the reference's
+    get_reaction_energy('electronic' / 'free') and get_reaction_barriers(...)[0]
+    (reaction.py:171-200), evaluated for all reactions in one device launch."""
+    from ..engine import evaluate_forms
+    keys = ('dErxn', 'dGrxn', 'dEa_fwd', 'dGa_fwd')
+    forms, slots = [], []
+    for r in sim_system.reactions.values():
+        e = r.energy_forms()
+        for k in keys:
+            slots.append(None if e[k] is None else len(forms))
+            if e[k] is not None:
+                forms.append(e[k])
+    states = list(sim_system.states.values())
+    vals = evaluate_forms(forms, T, p, states=states) if forms else []
+    out = []
+    for i, _ in enumerate(sim_system.reactions):
+        row = []
+        for k in range(len(keys)):
+            s = slots[i * len(keys) + k]
+            row.append(None if s is None else vals[s] * 1.0e3 * 96.485)
+        out.append(row)
+    return out
+
+
+def save_energies(sim_system, csv_path=''):
+    """presets.py:378-406: reaction_energies_and_barriers_<T>K_<p>bar.csv with
+    columns Reaction, dEr, dGr, dEa, dGa (J/mol) at params' T and p."""
+    import pandas as pd
+    _mkdir(csv_path)
+    T, p = sim_system.params['temperature'], sim_system.params['pressure']
+    rows = _reaction_energy_rows(sim_system, T, p)
+    df = pd.DataFrame(data=[[r] + v for r, v in zip(sim_system.reactions, rows)],
+                      columns=['Reaction', 'dEr (J/mol)', 'dGr (J/mol)', 'dEa (J/mol)', 'dGa (J/mol)'])
+    df.to_csv(csv_path + 'reaction_energies_and_barriers_%1.1fK_%1.1fbar.csv' % (T, p / bartoPa), index=False)
+
+
+def save_energies_temperatures(sim_system, temperatures, csv_path=''):
+    """presets.py:409-438: reaction_energies_and_barriers_<reaction>.csv, one row
+    per temperature.  As in the reference, params['temperature'] is left at the
+    last temperature."""
+    import pandas as pd
+    _mkdir(csv_path)
+    p = sim_system.params['pressure']
+    temps = [float(T) for T in np.ravel(temperatures)]
+    per_T = [_reaction_energy_rows(sim_system, T, p) for T in temps]
+    for i, r in enumerate(sim_system.reactions):
+        df = pd.DataFrame(data=[[T] + per_T[k][i] for k, T in enumerate(temps)],
+                          columns=['Temperature (K)', 'dEr (J/mol)', 'dGr (J/mol)', 'dEa (J/mol)', 'dGa (J/mol)'])
+        df.to_csv(csv_path + 'reaction_energies_and_barriers_%s.csv' % r, index=False)
+    if temps:
+        sim_system.params['temperature'] = temps[-1]
+
+
+def state_energy_table(sim_system, T=None, p=None):
+    """{state: [Gfree, Gelec, Gvibr, Grota, Gtran]} (eV) -- the values
+    State.calc_free_energy leaves on each state (state.py:367-386), in the row
+    order save_state_energies writes them.  A state whose free energy is given
+    in the input keeps its given components (None where absent)."""
+    from ..engine import evaluate_forms
+    T = sim_system.params['temperature'] if T is None else T
+    p = sim_system.params['pressure'] if p is None else p
+    names = sorted(sim_system.states)
+    forms, slots = [], {}
+    for s in names:
+        st = sim_system.states[s]
+        if st.Gfree is not None:
+            slots[s] = [len(forms)] + [None] * 4
+            forms.append(st.free_form())
+            continue
+        slots[s] = list(range(len(forms), len(forms) + 5))
+        forms += [st.free_form(), st.elec_form(), st.vib_form(), st.rot_form(), st.tran_form()]
+    vals = evaluate_forms(forms, T, p, states=[sim_system.states[s] for s in names]) if forms else []
+    out = {}
+    for s in names:
+        st = sim_system.states[s]
+        given = [None, st.Gelec, st.Gvibr, st.Grota, st.Gtran]
+        out[s] = [vals[k] if k is not None else (None if g is None else float(g))
+                  for k, g in zip(slots[s], given)]
+    return out
+
+
+def save_state_energies(sim_system, csv_path=''):
+    """presets.py:441-471: state_energies_<T>K_<p>bar.csv.  The reference writes
+    [Gfree, Gelec, Gvibr, Grota, Gtran] under the header Free, Electronic,
+    Vibrational, Translational, Rotational -- Grota sits in the
+    'Translational (eV)' column and Gtran in 'Rotational (eV)' -- and its
+    goldens (test/test_1.py:78-81) are read from those columns, so the same
+    placement is kept."""
+    import pandas as pd
+    _mkdir(csv_path)
+    T, p = sim_system.params['temperature'], sim_system.params['pressure']
+    tab = state_energy_table(sim_system, T, p)
+    df = pd.DataFrame(data=[[s] + tab[s] for s in sorted(sim_system.states)],
+                      columns=['State', 'Free (eV)', 'Electronic (eV)', 'Vibrational (eV)', 'Translational (eV)',
+                               'Rotational (eV)'])
+    df.to_csv(csv_path + 'state_energies_%1.1fK_%1.1fbar.csv' % (T, p / bartoPa), index=False)
+
+
+def get_tof_for_given_reactions(sim_system, tof_terms):
+    """presets.py:585-597: sum of (r_fwd - r_rev) over tof_terms at the last
+    transient state (sim_system.solution[-1]); the system's stored rates are
+    left as they were (the reference works on a deep copy)."""
+    if sim_system.solution is None:
+        raise RuntimeError('get_tof_for_given_reactions: run solve_odes() first')
+    keep = sim_system.rates
+    try:
+        rates = sim_system.reaction_terms(sim_system.solution[-1])
+    finally:
+        sim_system.rates = keep
+    names = list(sim_system.plan().all_reactions)
+    return float(sum(rates[names.index(r), 0] - rates[names.index(r), 1] for r in tof_terms if r in names))

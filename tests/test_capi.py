@@ -40,6 +40,29 @@ def test_header_enums_match_python_constants():
     assert len(names) + 1 == _lib.I_HDR
 
 
+def _struct_fields(txt, name):
+    """Member names of `typedef struct { ... } name;` in declaration order."""
+    body = re.search(r"typedef struct \{([^{}]*)\}\s*%s;" % name, txt).group(1)
+    out = []
+    for decl in body.split(';'):
+        decl = decl.strip()
+        if not decl:
+            continue
+        # "const double* T" / "double t0, t_end" / "int64_t ld_desc, s_desc"
+        first, *rest = [d.strip() for d in decl.split(',')]
+        out.append(first.replace('*', ' ').split()[-1])
+        out += [r.replace('*', ' ').split()[-1] for r in rest]
+    return out
+
+
+@pytest.mark.parametrize('cname, pyname', [('pck_conditions', 'Conditions'), ('pck_solve_params', 'SolveParams'),
+                                           ('pck_outputs', 'Outputs')])
+def test_struct_layouts_match_header(cname, pyname):
+    """The ctypes mirrors of the C-ABI structs list the header's members in order."""
+    txt = re.sub(r'/\*.*?\*/', '', open(HDR).read(), flags=re.S)
+    assert _struct_fields(txt, cname) == [f[0] for f in getattr(_lib, pyname)._fields_]
+
+
 def test_embedded_rtc_sources_match_headers():
     """The device headers hipRTC compiles network-specialised solvers from
     (csrc/rtc_sources.inc, written by build()) are the library's own."""

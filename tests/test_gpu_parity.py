@@ -485,6 +485,29 @@ def test_trajectory_dense_output_vs_oracle(P, inputs, which, tmp_path):
     assert len(glob.glob(str(out) + '/*.csv')) == 3
 
 
+@pytest.mark.parametrize('which', ['cstr', 'dmtm'])
+def test_trajectory_end_not_power_of_ten(P, inputs, which):
+    """times = [0, 7200]: 10**log10(7200) is one ulp above 7200, so the last
+    output sample used to lie past t_end and was never written.  The last row
+    of solve_odes() must be the solver's final state (the start of
+    find_steady's Newton, old_system.py:393-395) and no sample may be NaN."""
+    f = ('COOxReactor', 'input_Pd111.json') if which == 'cstr' else ('DMTM', 'input.json')
+    s = P.read_from_input_file(os.path.join(inputs, *f))
+    s.params.update(times=[0.0, 7200.0], nsteps=40)
+    sol = s.solve_odes()
+    assert s.times[-1] == 7200.0
+    assert np.all(np.isfinite(sol))
+    plan = s.plan()
+    r = s.solve_batch(T=[s.params['temperature']], t0=0.0, t_end=7200.0)
+    dyn = [plan.species.index(n) for n in plan.dyn]
+    np.testing.assert_allclose(sol[-1, dyn], r['y'][:, 0], rtol=1e-12, atol=1e-300)
+    # the device sampler also covers a grid that overshoots t_end by rounding
+    t_out = np.array([0.0, 3600.0, 7200.0 * (1.0 + 4e-16)])
+    rt = s.solve_batch(T=[s.params['temperature']], t0=0.0, t_end=7200.0, t_out=t_out)
+    assert np.all(np.isfinite(rt['traj']))
+    np.testing.assert_allclose(rt['traj'][-1, :, 0], r['y'][:, 0], rtol=1e-12, atol=1e-300)
+
+
 def test_run_parameters_generic_key_and_start_state(P, inputs):
     """run_parameters over a params key outside the batched four
     (presets.py:187-188 sets any key): one launch per value, each equal to a
