@@ -108,7 +108,17 @@ def cpu_baseline(config, n_points=160, workers=16, seed=0, budget_s=25.0):
     rng = np.random.default_rng(seed)
     pts = [(config, tuple(p)) for p in rng.uniform(0.0, 1.0, (n_points, 4))]
     ctx = mp.get_context('spawn')
-    pool = ctx.Pool(workers)
+    # one core per worker: the spawned interpreters inherit single-threaded BLAS
+    keep = {k: os.environ.get(k) for k in ('OMP_NUM_THREADS', 'OPENBLAS_NUM_THREADS', 'MKL_NUM_THREADS')}
+    os.environ.update({k: '1' for k in keep})
+    try:
+        pool = ctx.Pool(workers)
+    finally:
+        for k, v in keep.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     try:
         pool.map(_cpu_warm, range(workers))            # imports outside the timed sample
         t = time.time()
@@ -123,6 +133,25 @@ def cpu_baseline(config, n_points=160, workers=16, seed=0, budget_s=25.0):
     return done / dt, dt, done
 
 
+def host_cores():
+    """CPUs this process may use: the affinity mask, capped by a cgroup CPU
+    quota (cpu.max) when one is set."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, 'sched_getaffinity') else (os.cpu_count() or 1)
+    try:
+        q, per = open('/sys/fs/cgroup/cpu.max').read().split()[:2]
+        if q != 'max':
+            n = min(n, max(1, int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+# A one-GPU box is given 16 of the host's CPUs (the pool's rule for one GPU:
+# nproc / os.cpu_count() report the whole machine there); the CPU baseline runs
+# one worker per CPU of that share.
+BOX_CPU_SHARE = 16
+
+
 def _cpu_warm(_):
     from oracle import mk_oracle  # noqa: F401
     return 0
@@ -134,7 +163,9 @@ def _cpu_point(arg):
     from oracle import mk_oracle as O
     if config == 'volcano':
         spec = O.load_spec(os.path.join(INPUTS, 'COOxVolcano', 'input.json'))
-        return O.volcano_point(spec, -2.5 + 3.0 * u[0], -2.5 + 3.0 * u[1], steady=True, rtol=1e-8, atol=1e-10)['activity']
+        # the reference's volcano path: lsoda (input ode_solver 'ode') at the input tolerances, then the root
+        return O.volcano_point(spec, -2.5 + 3.0 * u[0], -2.5 + 3.0 * u[1], steady=True, rtol=1e-8, atol=1e-10,
+                               method='LSODA')['activity']
     if config == 'cstr':
         spec = O.load_spec(os.path.join(INPUTS, 'COOxReactor', 'input_Pd111.json'))
         m = O.ClassicModel(spec, T=423.0 + 200.0 * u[0])
@@ -250,6 +281,7 @@ def _outputs(torch, net, n, L, _ptr):
 def _solve_workload(wl, sim, net, plan, n, T, p, desc, tof_terms, steady, activity, t_end=None, rtol=None,
                     atol=None, args=None):
     import torch
+    from pycatkin_amd.classes.system import DEGENERATE_RETRY
     from pycatkin_amd import _lib as L
     from pycatkin_amd.engine import _ptr
     Tt, pp, d, fx, y0, inflow = sim._inputs(net, plan, n, T, p, desc, None, None, None)
@@ -258,7 +290,8 @@ def _solve_workload(wl, sim, net, plan, n, T, p, desc, tof_terms, steady, activi
     wl.prm = net.params(t0=times[0], t_end=times[-1] if t_end is None else t_end,
                         rtol=sim.params['rtol'] if rtol is None else rtol,
                         atol=sim.params['atol'] if atol is None else atol, max_steps=args.max_steps,
-                        newton=steady and not args.no_newton, newton_iters=30, activity=activity)
+                        newton=steady and not args.no_newton, newton_iters=30, activity=activity,
+                        retry=None if args.no_retry else DEGENERATE_RETRY)
     wl.out, wl.o = _outputs(torch, net, n, L, _ptr)
     wl.kf = torch.empty((max(net.NRXN, 1), max(n, 1)), dtype=torch.float64, device='cuda')
     wl.kr = torch.empty_like(wl.kf)
@@ -280,6 +313,7 @@ def _solve_workload(wl, sim, net, plan, n, T, p, desc, tof_terms, steady, activi
 
 def volcano_workload(args, rank, world):
     import pycatkin_amd as P
+    from pycatkin_amd.classes.system import DEGENERATE_RETRY
     from pycatkin_amd.functions.volcano import set_volcano_energies, tile_order
     from pycatkin_amd.parallel import weak_grid_rows
     wl = Workload()
@@ -311,9 +345,10 @@ def volcano_workload(args, rank, world):
                     ('CO_ox',), True, True, args=args)
     wl.tag = 'volcano %dx%d %s' % (wl.global_grid[0], wl.global_grid[1], args.order)
     wl.config = {'workload': 'COOxVolcano %dx%d (E_CO x E_O) grid, %s over %d GPU(s): %d E_CO rows x %d E_O per rank, '
-                             'T=600 K, t_end=3600 s, rtol 1e-8 / atol 1e-10, Newton steady-state polish, activity'
+                             'T=600 K, t_end=3600 s, rtol 1e-8 / atol 1e-10, Newton steady-state polish, activity; '
+                             'degenerate roots re-integrated to t_end at rtol %%g / atol %%g in the same launch'
                              % (wl.global_grid[0], wl.global_grid[1], 'sharded' if args.scaling == 'strong'
-                                else 'one grid share per GPU', world, rows, G),
+                                else 'one grid share per GPU', world, rows, G) % DEGENERATE_RETRY,
                  'global_grid': list(wl.global_grid), 'grid_per_gpu': [rows, G],
                  'parallelism': 'dp%d' % world, 'shard': 'cyclic E_CO rows',
                  'order': 'row' if wl.perm is None else 'tile %s' % args.tile}
@@ -459,7 +494,7 @@ def cpu_standin_workload(args, rank, world):
     return wl
 
 
-def main(argv=None):
+def build_parser():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=10)
@@ -472,6 +507,8 @@ def main(argv=None):
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-points', type=int, default=160)
     ap.add_argument('--no-newton', action='store_true', help='A/B diagnostic: transient only (not the bench workload)')
+    ap.add_argument('--no-retry', action='store_true',
+                    help='A/B diagnostic: degenerate roots keep the first transient (not the bench workload)')
     ap.add_argument('--emulate', default=None, metavar='R/N',
                     help='single-GPU A/B: solve the shard rank R of N would own, without a process group')
     ap.add_argument('--tile', default='16x4', help='patch shape (rows x cols) of --order tile')
@@ -480,8 +517,12 @@ def main(argv=None):
     ap.add_argument('--runtime-plan', action='store_true',
                     help='A/B: force the runtime-plan solver instead of the compiled-in network')
     ap.add_argument('--device', choices=('gpu', 'cpu-standin'), default='gpu', help=argparse.SUPPRESS)
+    return ap
+
+
+def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
-    args = ap.parse_args(argv)
+    args = build_parser().parse_args(argv)
 
     if 'WORLD_SIZE' not in os.environ and args.gpus > 1:
         if args.emulate:
@@ -601,20 +642,23 @@ def main(argv=None):
                     '+ 128 x FMA fp64 wave instructions of the committed PMC profile of this workload)',
                     'integrator_steps': steps_local, 'lane_efficiency': lane_eff}
             if world == 1 and not args.no_cpu_baseline:
-                workers = min(16, os.cpu_count() or 1)
+                avail = host_cores()
+                workers = min(BOX_CPU_SHARE, avail)
                 log('cpu baseline: %d points, %d workers' % (args.cpu_points, workers))
                 v, dt, done = cpu_baseline(args.config, args.cpu_points, workers)
                 cpu_line = dict(value=v, unit='%s/s' % wl.units, cores=workers, kind='port',
                                 sample='%d random units of the same %s workload solved in %.1f s by the oracle '
-                                       '(numpy/scipy restatement of the reference path), %d worker processes'
-                                       % (done, args.config, dt, workers))
+                                       '(numpy/scipy restatement of the reference path), %d single-threaded worker '
+                                       'processes = the one-GPU box\'s CPU share (affinity/cgroup show %d, '
+                                       'os.cpu_count() %d for the whole host)'
+                                       % (done, args.config, dt, workers, avail, os.cpu_count() or 0))
         line = {
             'metric': METRIC if args.config == 'volcano' else
             '%s/sec (whole node), BASELINE config %s' % (wl.units, args.config),
             'value': value, 'unit': '%s/s' % wl.units, 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
             'ms_per_step': per_step * 1e3, 'higher_is_better': True, 'scaling': args.scaling, 'vs_baseline': None,
             'dtype': 'f64', 'data': wl.data, 'config': wl.config, 'roofline': roof, 'cpu_baseline': cpu_line,
-            'status': {'regular_root': n_ok, 'degenerate_root_transient_kept': n_degen, 'failed': n_fail,
+            'status': {'regular_root': n_ok, 'degenerate_root_tight_transient': n_degen, 'failed': n_fail,
                        'units': n_total},
         }
         if args.emulate:

@@ -712,11 +712,13 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
         PCK_PH(2, (k6 = grp_solve<NSP, G>(x, F, keep * (fu + ih * (C61 * k1 + C62 * k2 + C63 * k3 + C64 * k4 +
                                                                      C65 * k5)))));
         u += k6;
-        const bool fin_l = !x.row || (isfinite(u) && isfinite(k6));
-        const double fin = gmin<G>(fin_l ? 1.0 : 0.0);
         const double sc = atol + rtol * fmax(fabs(y), fabs(u));
         const double r = k6 * __builtin_amdgcn_rcp(sc);     // error weight: the v_rcp_f64 estimate suffices
-        const double s = gsum<G>(x.row ? r * r : 0.0);
+        // the finiteness test rides on the error sum: a non-finite stage value
+        // makes u (which includes k6) non-finite, and 0 * (inf or NaN) is NaN;
+        // for finite u the added term is an exact zero
+        const double s = gsum<G>(x.row ? r * r + 0.0 * u : 0.0);
+        const double fin = (s == s) ? 1.0 : 0.0;
         const double q = (fin > 0.0) ? s * invNS : INFINITY;     // en^2
         // positivity (mass-action concentrations stay >= -atol): a step that
         // drives a component below -atol is rejected and retried at the

@@ -468,17 +468,19 @@ __device__ PCK_LANE_INLINE int integrate(const P& p, const Lane<P::NS>& L, const
             k5[i] = fu[i] + ih * (C61 * k1[i] + C62 * k2[i] + C63 * k3[i] + C64 * k4[i] + C65 * k5[i]);
         if (PCK_CONS_ROWS && crows) cons_zero(p, k5);
         lu_solve<NS>(W, piv, sw, k5);
-        bool finite = true;
-        double s = 0.0, umin = INFINITY;
+        double s = 0.0, umin = INFINITY, usum = 0.0;
 #pragma unroll
         for (int i = 0; i < NS; ++i) {
             u[i] += k5[i];
-            finite = finite && isfinite(u[i]) && isfinite(k5[i]);
+            usum += u[i];
             umin = fmin(umin, u[i]);
             const double sc = atol + rtol * fmax(fabs(y[i]), fabs(u[i]));
             const double r = k5[i] * __builtin_amdgcn_rcp(sc);   // error weight: the v_rcp_f64 estimate suffices
             s += r * r;
         }
+        // one finiteness test for the step: a non-finite stage value makes u
+        // (which includes k6) non-finite, hence usum, and 0 * (inf or NaN) is NaN
+        const bool finite = (0.0 * usum == 0.0);
         const double q = finite ? s * (1.0 / NS) : INFINITY;    // en^2
         // positivity (mass-action concentrations stay >= -atol): a step that
         // drives a component below -atol is rejected and retried at the
@@ -531,10 +533,9 @@ __device__ PCK_LANE_INLINE int integrate(const P& p, const Lane<P::NS>& L, const
             // the error estimate rejects steps forever (tools/rodas_mirror.py
             // CLIPMODE, DESIGN.md "Positivity").  The common case costs one
             // min over the state and one wave vote.
-            double ymin = y[0];
-#pragma unroll
-            for (int i = 1; i < NS; ++i) ymin = fmin(ymin, y[i]);
-            if (PCK_POSITIVITY && __any(ymin < 0.0)) {        // rare: one wave-uniform branch
+            // the site-balance rescaling multiplies by a positive factor, so the
+            // accepted state has a negative component exactly where u did
+            if (PCK_POSITIVITY && __any(umin < 0.0)) {        // rare: one wave-uniform branch
                 bool negf = false;
 #pragma unroll
                 for (int i = 0; i < NS; ++i)

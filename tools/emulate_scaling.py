@@ -1,0 +1,70 @@
+"""Predicted multi-GPU curve of the headline bench from one GPU.
+
+The ranks of `bench.py --gpus N` share nothing in the timed region (cyclic
+E_CO rows of the grid, no collective until after timing), so rank r's step
+time on an 8-GPU node is the time of its shard alone on one GPU: this runs
+every shard r of N = 1, 2, 4, 8 in one process (the bench's own workload
+builder, HIP-event timing on the solve stream) and reports, per N, the
+per-rank times, the max over ranks (the bench's step time) and the whole-node
+value = units / max.  Strong scaling (default, BASELINE configs[2]: the fixed
+1024 x 1024 grid) and, for N = 8, the weak layout (1024 x 1024 per rank).
+
+    python tools/emulate_scaling.py [--steps 3] > gpurun_out/emulate_scaling.json
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def shard_ms(bench, torch, scaling, rank, world, steps):
+    args = bench.build_parser().parse_args(['--scaling', scaling])
+    wl = bench.volcano_workload(args, rank, world)
+    sp = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    wl.step(sp)
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(steps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        wl.step(sp)
+        b.record()
+        torch.cuda.synchronize()
+        ts.append(a.elapsed_time(b))
+    st = wl.status().cpu().numpy()
+    ns = wl.nsteps().cpu().numpy().astype(np.int64)
+    return dict(rank=rank, ms=float(np.median(ts)), units=int(wl.n_local), steps_max=int(ns.max()),
+                steps_mean=float(ns.mean()), degenerate=int((st == 4).sum()))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--steps', type=int, default=3)
+    a = ap.parse_args()
+    import torch
+    import bench
+    out = []
+    for scaling, worlds in (('strong', (1, 2, 4, 8)), ('weak', (8,))):
+        for N in worlds:
+            ranks = [shard_ms(bench, torch, scaling, r, N, a.steps) for r in range(N)]
+            t = max(x['ms'] for x in ranks)
+            units = sum(x['units'] for x in ranks)
+            line = dict(scaling=scaling, n_gpus=N, rank_ms=[x['ms'] for x in ranks], max_rank_ms=t,
+                        predicted_value=units / (t * 1e-3), units=units, ranks=ranks)
+            print(json.dumps(line), flush=True)
+            out.append(line)
+    base = [x for x in out if x['scaling'] == 'strong' and x['n_gpus'] == 1][0]['predicted_value']
+    for x in out:
+        x['predicted_speedup_vs_1'] = x['predicted_value'] / base
+    print(json.dumps(dict(summary=[{k: x[k] for k in ('scaling', 'n_gpus', 'max_rank_ms', 'predicted_value',
+                                                     'predicted_speedup_vs_1')} for x in out])))
+
+
+if __name__ == '__main__':
+    main()
