@@ -145,7 +145,9 @@ typedef struct {
     int64_t n_out;         /*   the state at each is written to pck_outputs.traj (dense output) */
     double retry_rtol;     /* with newton: a condition whose polish meets a degenerate root */
     double retry_atol;     /*   (PCK_ST_NEWTON) is integrated again, t0..t_end, at these tolerances,
-                            *   in the same launch (0: off); its y / tof become that transient end,
+                            *   by a second launch over the compacted list of such conditions on
+                            *   the same stream (pck_solve only; 0: off); its y / tof become that
+                            *   transient end,
                             *   the reference's System.activity semantics (old_system.py:517-529),
                             *   status stays PCK_ST_NEWTON (or the retry's failure status) and
                             *   nsteps adds the retry's steps */

@@ -232,7 +232,11 @@ class System:
         species enters a side of a reaction with exponent 1 (a repeated species
         with its count), so d(k prod c)/d y_k = k prod(others) (x p for a gas):
         the rate of that side with y_k set to 1 -- one device launch evaluates
-        the rates at all n_species such compositions."""
+        the rates at all n_species such compositions.  The reference's P_term
+        (system.py:478-484) multiplies by p only when ANOTHER species of the
+        side is a gas, so the column of a gas species itself carries no p:
+        that column is divided by p here to return the reference's matrix
+        (the device integrators use the exact derivative)."""
         self._patched_eval()
         y = np.asarray(y, float).ravel()
         n = len(y)
@@ -248,6 +252,8 @@ class System:
                     cnt = lst.count(i)
                     # side rate at y_i = 1 is k prod(others) y_i^0 -> times cnt y_i^(cnt-1)
                     out[j, i] = sgn * r[j, i] * (cnt * y[i] ** (cnt - 1) if cnt > 1 else 1.0)
+                    if i in self.gas_indices:
+                        out[j, i] /= float(self.p)
         return out
 
     def get_jacobian(self, y):

@@ -729,7 +729,15 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
         if (q <= 1.0 && pf >= 1.0) {
             const double t_old = t, y_old = y;
             t = last ? t_end : t + h;
-            y = x.row ? u : 0.0;
+            // clamped-state rates: a negative component enters every rate as
+            // 0, so the clamped flow never leaves y >= 0 and a negative is
+            // pure discretisation error.  Kept, it also makes the state and
+            // the Jacobian (taken at max(y, 0)) disagree: on synthetic
+            // condition 39547 a -5e-11 component held the error estimate at
+            // the controller's fixed point (en^2 = 0.9^8, h = 0.034 s) for
+            // 99 160 steps (profiles/r2/synthetic/trace_39547.log).  Set to 0
+            // it changes no rate -- they already saw 0.
+            y = x.row ? (CLAMP ? fmax(u, 0.0) : u) : 0.0;
 #pragma unroll
             for (int l = 0; l < PCK_MAX_CONS; ++l) {
                 if (l < nv.NCONS) {
@@ -777,6 +785,41 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
             if (x.row) to.y[((int64_t)ko * NS + x.gl) * to.ld + to.c] = y;
     }
     return PCK_ST_OK;
+}
+
+// forward + reverse rate of a record's reaction (its gross flux)
+__device__ __forceinline__ double rec_gross(const uint4& rec, double a, double b, const double* c) {
+#pragma unroll
+    for (int k = 0; k < PCK_GRP_NPMAX; ++k) {
+        const int f = rx_field(rec, k);
+        const double x = c[f & 63];
+        const int ef = (f >> 6) & 31, er = f >> 11;
+        a *= spow(x, ef);
+        b *= spow(x, er);
+    }
+    return fabs(a) + fabs(b);
+}
+
+// mk_solver.h: resolved -- every non-pivot species balance within
+// PCK_BALANCE_TOL of its gross flux (group-uniform result)
+template <int NSP, int G>
+__device__ __forceinline__ bool grp_resolved(const NetView& nv, const GrpView& g, const Grp<NSP>& x, double y) {
+    const double f = grp_rhs<NSP, G>(g, x, y);
+    wsync();                                   // the rows' reads of the net rates are done
+    for (int r = x.gl; r < x.R; r += G) x.d[r] = rec_gross(g.rx[r], x.kf[r], x.kr[r], x.c);
+    wsync();
+    double gr = 0.0;
+    if (x.row) {
+        for (int e = x.rb; e < x.re; ++e) {
+            const uint4 q = g.ent[e];
+            gr += fabs(ent_s(q)) * x.d[ent_r(q)];
+        }
+        gr = gr * fabs(x.rs) + fabs(x.fl) * (fabs(x.in) + fabs(y));
+    }
+    bool pv = false;
+    for (int l = 0; l < nv.NCONS; ++l) pv = pv || (nv.cpiv[l] == x.gl);
+    const bool bad = x.row && !pv && !(fabs(f) <= PCK_BALANCE_TOL * gr);
+    return gmaxi<G>(bad ? 1 : 0) == 0;
 }
 
 // Newton steady-state polish (same rules as mk_solver.h: newton)
@@ -842,6 +885,7 @@ __device__ __forceinline__ int grp_newton(const NetView& nv, const GrpView& gv, 
     }
     if (!conv) return PCK_ST_NEWTON;
     if (gmin<G>((x.row && z < 0.0) ? -1.0 : 1.0) < 0.0) return PCK_ST_NEWTON;
+    if (!grp_resolved<NSP, G>(nv, gv, x, z)) return PCK_ST_NEWTON;   // converged in absolute terms only
     y = z;
     return PCK_ST_OK;
 }
@@ -933,7 +977,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 64
     extern __shared__ double lds[];
     const int grp = threadIdx.x / G;
     const int64_t v = (int64_t)blockIdx.x * (64 / G) + grp;
-    const int64_t slot = v / ga.M;
+    const int64_t slot = cond_of(a, v, ga.M, cv.n);
     const int q = (int)(v % ga.M);
     const int R1 = nv.NRXN > 0 ? nv.NRXN : 1, NE1 = gv.NE > 0 ? gv.NE : 1;
     GrpView gl = gv;                                // TAB: the tables, copied to LDS by the whole block (one wave)
@@ -963,25 +1007,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 64
     int ns = 0;
     TrajOut to{a.t_out, a.n_out, a.traj, a.ld_traj, c};
     LU<NSP> F;                  // one factorisation storage for the transient and the Newton polish
-    // transient, polish and -- for a degenerate root -- the retry transient at
-    // a.retry_rtol / retry_atol (mk_solver.h: solve_lane; group-uniform)
-    int st = PCK_ST_OK;
-    double rtol = a.rtol, atol = a.atol;
-    for (int pass = 0; pass < 2; ++pass) {
-        y = x.row ? cv.y0[x.gl * cv.ld_y0 + c * cv.s_y0] : 0.0;
-        int nsp = 0;
-        st = grp_integrate<NSP, G, P, TRAJ>(nv, gl, x, y, a.t0, a.t_end, rtol, atol, a.max_steps, nsp,
+    // transient and polish (a degenerate root's retry transient is a second
+    // launch over the compacted list, mk_solver.h: SolveArgs::idx)
+    y = x.row ? cv.y0[x.gl * cv.ld_y0 + c * cv.s_y0] : 0.0;
+    int st = grp_integrate<NSP, G, P, TRAJ>(nv, gl, x, y, a.t0, a.t_end, a.rtol, a.atol, a.max_steps, ns,
                                             a.cons_rows != 0, to, F);
-        ns += nsp;
-        if (pass == 1) {
-            if (st == PCK_ST_OK) st = PCK_ST_NEWTON;
-            break;
-        }
-        if (st == PCK_ST_OK && a.newton) st = grp_newton<NSP, G, P>(nv, gl, x, y, a.newton_iters, F);
-        if (!(st == PCK_ST_NEWTON && a.retry_rtol > 0.0)) break;
-        rtol = a.retry_rtol;
-        atol = a.retry_atol;
-    }
+    if (st == PCK_ST_OK && a.newton) st = grp_newton<NSP, G, P>(nv, gl, x, y, a.newton_iters, F);
+    if (a.retry_pass && st == PCK_ST_OK) st = PCK_ST_NEWTON;
     const double tof = grp_tof<NSP, G>(nv, gl, x, y);
     const bool fin = gmin<G>((!x.row || isfinite(y)) ? 1.0 : 0.0) > 0.0 && isfinite(tof);
     if (!fin && st == PCK_ST_OK) st = PCK_ST_NONFINITE;
@@ -997,7 +1029,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 64
     if (x.gl == 0) {
         if (a.tof) a.tof[c] = a.want_activity ? (log((hP * tof) / (kB * T)) * (Rgas * T)) * 1.0e-3 / eVtokJ : tof;
         if (a.status) a.status[c] = st;
-        if (a.nsteps) a.nsteps[c] = ns;
+        if (a.nsteps) a.nsteps[c] = a.retry_pass ? a.nsteps[c] + ns : ns;
     }
 }
 

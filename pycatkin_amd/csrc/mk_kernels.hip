@@ -633,6 +633,25 @@ static int check_params(const pck_solve_params* prm) {
     return PCK_OK;
 }
 
+// Retry list: the indices c < n with status[c] == want, appended per
+// wavefront (one ballot, one vector atomic on the list length per wave that
+// has any), so the 64 conditions of a grid patch stay together in the list.
+// The list's order across wavefronts follows the atomics; every lane's solve
+// is independent of which lanes share its wavefront, so results do not
+// depend on it.
+__global__ void __launch_bounds__(256) k_select_status(int64_t n, const int32_t* status, int32_t want,
+                                                       int64_t* idx, int32_t* cnt) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool f = (c < n) && status[c] == want;
+    const unsigned long long m = __ballot(f);
+    if (m == 0ull) return;                             // wave-uniform
+    const int lane = threadIdx.x & 63;
+    int base = 0;
+    if (lane == 0) base = atomicAdd(cnt, (int)__popcll(m));
+    base = __shfl(base, 0, 64);
+    if (f) idx[base + __popcll(m & ((1ull << lane) - 1ull))] = c;
+}
+
 // One solver launch over the batch (lane or lane-group path).
 static int run_solver(const pck_network* net, const pck_conditions* cond, const SolveArgs& a_in, bool grp,
                       GrpArgs& ga, bool traj, const double* kf, const double* kr, hipStream_t s) {
@@ -751,9 +770,10 @@ static int launch_solve(const pck_network* net, const pck_conditions* cond, cons
     a.t0 = prm->t0; a.t_end = prm->t_end; a.rtol = prm->rtol; a.atol = prm->atol; a.eps = prm->drc_eps;
     a.max_steps = prm->max_steps; a.newton = prm->newton; a.newton_iters = prm->newton_iters;
     a.want_activity = prm->want_activity;
-    // degenerate roots (status 4) re-integrated in the same launch (mk_solver.h: solve_lane)
-    a.retry_rtol = prm->newton ? prm->retry_rtol : 0.0;
-    a.retry_atol = prm->retry_atol;
+    a.idx = nullptr; a.nidx = nullptr; a.retry_pass = 0;
+    // degenerate roots (status 4) are re-integrated by a second launch over
+    // their compacted list (pck_solve only: G == 1, no DRC groups)
+    const bool retry = prm->newton && prm->retry_rtol > 0.0 && !drc_groups && a.G == 1;
     const bool traj = (prm->n_out > 0 && a.traj != nullptr);
     if (traj) {
         if (!prm->t_out) return fail(PCK_E_ARG, "n_out > 0 without t_out%s", "");
@@ -788,8 +808,37 @@ static int launch_solve(const pck_network* net, const pck_conditions* cond, cons
         ga.stbuf = (int32_t*)(ga.tofbuf + m);
         ga.nsbuf = ga.stbuf + m;
     }
+    StreamScratch rscr;
+    if (retry) {
+        // the retry list (int64 per condition), its length, and a status
+        // array when the caller passed none
+        const size_t bytes = sizeof(int64_t) * (size_t)n + 64 + (a.status ? 0 : sizeof(int32_t) * (size_t)n);
+        rc = salloc(rscr, bytes, s);
+        if (rc) return rc;
+        if (!a.status) a.status = (int32_t*)(rscr.as<char>() + sizeof(int64_t) * (size_t)n + 64);
+    }
     rc = run_solver(net, cond, a, grp, ga, traj, kf, kr, s);
     if (rc) return rc;
+    if (retry) {
+        int64_t* idx = rscr.as<int64_t>();
+        int32_t* cnt = (int32_t*)(idx + n);
+        HIPCHK(hipMemsetAsync(cnt, 0, sizeof(int32_t), s));
+        hipLaunchKernelGGL(k_select_status, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, a.status,
+                           (int32_t)PCK_ST_NEWTON, idx, cnt);
+        HIPCHK(hipGetLastError());
+        // pass 1: the same grid (the list's length stays on the device); lanes
+        // past *cnt idle at once
+        SolveArgs r = a;
+        r.rtol = prm->retry_rtol;
+        r.atol = prm->retry_atol;
+        r.newton = 0;
+        r.idx = idx;
+        r.nidx = cnt;
+        r.retry_pass = 1;
+        if (!r.nsteps) r.nsteps = nullptr;
+        rc = run_solver(net, cond, r, grp, ga, traj, kf, kr, s);
+        if (rc) return rc;
+    }
     if (drc_groups) {
         hipLaunchKernelGGL(k_drc_combine, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, R, a.eps,
                            ga.tofbuf, ga.stbuf, ga.nsbuf, a.xi, a.ld_xi, a.tof0, a.status, a.nsteps);

@@ -578,6 +578,55 @@ __device__ PCK_LANE_INLINE int integrate(const P& p, const Lane<P::NS>& L, const
     return PCK_ST_OK;
 }
 
+// Is y a root to working precision?  Every species balance that is not a
+// conservation pivot must hold to PCK_BALANCE_TOL of its gross flux
+// (sum over reactions of |S_ij| (r_fwd + r_rev) times the row scale, plus
+// the CSTR flow terms).  Newton's step test holds components below 1e-12 of
+// the largest only to an absolute floor, so on an O-poisoned volcano node it
+// can stop at coverages of 1e-41 that balance nothing (every such equation
+// off by ~100 % of its own flux: the trivial poisoned root approached, TOF ~
+// 1e-36 and undetermined); resolved roots balance to <= 2e-14 (the 2 229
+// regular nodes of tests/golden/volcano_fixture.npz).
+#ifndef PCK_BALANCE_TOL
+#define PCK_BALANCE_TOL 1e-8
+#endif
+template <class P, class K>
+__device__ __forceinline__ bool resolved(const P& p, const Lane<P::NS>& L, const K& k, const double (&y)[P::NS]) {
+    constexpr int NS = P::NS;
+    double c[NS], f[NS], g[NS];
+#pragma unroll
+    for (int i = 0; i < NS; ++i) { c[i] = p.cf(i) * y[i]; f[i] = 0.0; g[i] = 0.0; }
+    for_rxn(p, [&](int j) {
+        double rf = k.f(j), rr = k.r(j);
+#pragma unroll
+        for (int i = 0; i < NS; ++i) {
+            if (p.ef(j, i)) rf *= ipow(c[i], p.ef(j, i));
+            if (p.er(j, i)) rr *= ipow(c[i], p.er(j, i));
+        }
+        const double net = rf - rr, gross = fabs(rf) + fabs(rr);
+#pragma unroll
+        for (int i = 0; i < NS; ++i) {
+            const double s = p.S(i, j);
+            if (s != 0.0) { f[i] += s * net; g[i] += fabs(s) * gross; }
+        }
+    });
+    bool ok = true;
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+        const double rs = (p.rsT(i) != 0.0) ? p.rs0(i) + p.rsT(i) * L.T : p.rs0(i);
+        f[i] *= rs;
+        g[i] *= fabs(rs);
+        if (p.fl(i) != 0.0) {
+            f[i] += p.fl(i) * (L.ins[i * L.ks] - y[i]);
+            g[i] += fabs(p.fl(i)) * (fabs(L.ins[i * L.ks]) + fabs(y[i]));
+        }
+        bool pv = false;
+        for (int l = 0; l < p.ncons(); ++l) pv = pv || (p.cpiv(l) == i);
+        ok = ok && (pv || fabs(f[i]) <= PCK_BALANCE_TOL * g[i]);
+    }
+    return ok;
+}
+
 // Newton on f(y) = 0 with the plan's conservation laws replacing their pivot
 // rows (old_system.py:385-468 polishes with scipy least_squares; a regular
 // root it converges to is the same).  Rows are equilibrated; a multiplicity
@@ -667,6 +716,7 @@ __device__ PCK_LANE_INLINE int newton(const P& p, const Lane<P::NS>& L, const K&
 #pragma unroll
     for (int i = 0; i < NS; ++i)
         if (z[i] < 0.0) return PCK_ST_NEWTON;
+    if (!resolved(p, L, k, z)) return PCK_ST_NEWTON;   // converged in absolute terms only
 #pragma unroll
     for (int i = 0; i < NS; ++i) y[i] = z[i];
     return PCK_ST_OK;
@@ -752,38 +802,38 @@ struct SolveArgs {
     int cons_rows;                             // conservation rows in the stage systems (A/B: PCK_CONS_ROWS=1)
     const double* t_out; int n_out;            // trajectory sample times (k_solve<P, true>)
     double* traj; int64_t ld_traj;             // [n_out][NS][ld_traj]
-    // degenerate-root retry (pck_solve_params.retry_rtol; 0 = off): a lane
-    // whose polish ends in PCK_ST_NEWTON integrates again from y0 at these
-    // tolerances, in the same launch, and reports that transient end
-    double retry_rtol, retry_atol;
+    // degenerate-root retry (pck_solve_params.retry_rtol), a second launch
+    // over the compacted list of the conditions whose polish ended in
+    // PCK_ST_NEWTON (mk_kernels.hip: launch_solve): lane i solves condition
+    // idx[i] for i < *nidx, adds its steps to nsteps[c] and reports a
+    // completed transient as PCK_ST_NEWTON.  idx == nullptr: lane i solves
+    // condition i / G.  (Round 3 first ran the retry inside the first launch;
+    // the pass loop kept ~70 more VGPRs live in every solver kernel -- the
+    // volcano kernel went from 158 to 227, i.e. from 3 to 2 waves per SIMD.)
+    const int64_t* idx; const int32_t* nidx;
+    int retry_pass;
 };
 
-// One condition's solve: transient, optional Newton polish and, for a
-// degenerate root, the retry transient (the pass loop keeps one inlined copy
-// of the integrator).  The lanes of a wave run pass 0 together; the lanes that
-// retry start pass 1 together, so the integrator's wave-uniform step counter
-// stays uniform.  Returns the status; ns = steps of both passes.
+// One condition's solve: transient from y0, then (with a.newton) the Newton
+// polish.  Returns the status; ns = integrator steps.
 template <bool TRAJ, class P, class K>
 __device__ __forceinline__ int solve_lane(const P& p, const Lane<P::NS>& L, const K& k, const CondView& cv,
                                           int64_t c, const SolveArgs& a, double (&y)[P::NS], int& ns,
                                           const TrajOut& to) {
     constexpr int NS = P::NS;
-    double rtol = a.rtol, atol = a.atol;
-    int st = PCK_ST_OK;
-    ns = 0;
-    for (int pass = 0; pass < 2; ++pass) {
 #pragma unroll
-        for (int i = 0; i < NS; ++i) y[i] = cv.y0[i * cv.ld_y0 + c * cv.s_y0];
-        int nsp = 0;
-        st = integrate<TRAJ>(p, L, k, y, a.t0, a.t_end, rtol, atol, a.max_steps, nsp, a.cons_rows != 0, to);
-        ns += nsp;
-        if (pass == 1) return (st == PCK_ST_OK) ? PCK_ST_NEWTON : st;
-        if (st == PCK_ST_OK && a.newton) st = newton(p, L, k, y, a.newton_iters);
-        if (!(st == PCK_ST_NEWTON && a.retry_rtol > 0.0)) break;
-        rtol = a.retry_rtol;
-        atol = a.retry_atol;
-    }
+    for (int i = 0; i < NS; ++i) y[i] = cv.y0[i * cv.ld_y0 + c * cv.s_y0];
+    int st = integrate<TRAJ>(p, L, k, y, a.t0, a.t_end, a.rtol, a.atol, a.max_steps, ns, a.cons_rows != 0, to);
+    if (st == PCK_ST_OK && a.newton) st = newton(p, L, k, y, a.newton_iters);
     return st;
+}
+
+// condition of a lane (or lane group) v: v / G, or the retry list's entry
+// (cv.n past the list's end: the lane idles)
+__device__ __forceinline__ int64_t cond_of(const SolveArgs& a, int64_t v, int G, int64_t n) {
+    if (!a.idx) return v / G;
+    const int64_t m = *a.nidx;
+    return (v < m) ? a.idx[v] : n;
 }
 
 template <class P>
@@ -813,7 +863,7 @@ __global__ void __launch_bounds__(PCK_SOLVE_BLOCK) __attribute__((amdgpu_waves_p
     extern __shared__ double lds[];
     const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int G = a.G;
-    const int64_t c = gid / G;
+    const int64_t c = cond_of(a, gid, G, cv.n);
     const int q = (int)(gid % G);
     const int R = nv.NRXN;
     P p(nv);
@@ -855,8 +905,9 @@ __global__ void __launch_bounds__(PCK_SOLVE_BLOCK) __attribute__((amdgpu_waves_p
                 // old_system.py:526-527
                 a.tof[c] = a.want_activity ? (log((hP * tof) / (kB * T)) * (Rgas * T)) * 1.0e-3 / eVtokJ : tof;
             }
+            if (a.retry_pass && st == PCK_ST_OK) st = PCK_ST_NEWTON;   // the transient of a degenerate root
             if (a.status) a.status[c] = st;
-            if (a.nsteps) a.nsteps[c] = ns;
+            if (a.nsteps) a.nsteps[c] = a.retry_pass ? a.nsteps[c] + ns : ns;
         }
     }
     if (drc) {

@@ -36,8 +36,8 @@ def test_launcher_world2(scaling, grid):
     assert st['units'] == grid[0] * grid[1]
     local = grid[0] * 32 // 2
     exp_degen = sum(sum(1 for i in range(local) if (i + r) % 7 == 0) for r in range(2))
-    assert st['degenerate_root_transient_kept'] == exp_degen
-    assert st['regular_root'] + st['degenerate_root_transient_kept'] + st['failed'] == st['units']
+    assert st['degenerate_root_tight_transient'] == exp_degen
+    assert st['regular_root'] + st['degenerate_root_tight_transient'] + st['failed'] == st['units']
     assert line['value'] > 0
 
 

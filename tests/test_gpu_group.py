@@ -417,6 +417,10 @@ def test_ch4_patched_api_vs_oracle(P, inputs):
     Jf = s.get_jacobian(y)
     Jo = m.jacobian(y)
     np.testing.assert_allclose(Jf[:, m.ngas:], Jo[:, m.ngas:], rtol=1e-10, atol=1e-12 * np.abs(Jo).max())
+    # gas columns as the reference returns them: P_term = p only for the OTHER
+    # species of a side (system.py:478-484), so the exact column divided by p
+    np.testing.assert_allclose(Jf[:, :m.ngas], Jo[:, :m.ngas] / float(s.p), rtol=1e-10,
+                               atol=1e-12 * np.abs(Jo).max())
     rates = s._calc_rates(y)
     assert rates.shape == (len(s.rate_map), 2)
     np.testing.assert_allclose(s.reaction_matrix @ (rates[:, 0] - rates[:, 1]), m.dydt(y), rtol=1e-10,

@@ -8,6 +8,7 @@
 #
 #   tests              pytest -m gpu (whole suite)           -> OUT/tests.log
 #   tests:EXPR         pytest -m gpu -k EXPR                 -> OUT/tests.log (appended)
+#   testsall[:EXPR]    the same without -x (every failure)   -> OUT/tests.log (appended)
 #   smoke              __graft_entry__.smoke()               -> OUT/smoke.log
 #   bench:ARGS         python bench.py ARGS (',' = ' ')      -> OUT/bench_<n>.json / .err
 #   py:SCRIPT,ARGS     python SCRIPT ARGS                    -> OUT/py_<n>.log
@@ -26,9 +27,10 @@ for step in "$@"; do
   [ "$kind" != "$step" ] && arg=${step#*:}
   echo "[gpu_steps] $(date +%T) step $k: $step" | tee -a gpurun_out/$OUT/steps.log
   case $kind in
-    tests)
+    tests|testsall)
       if [ -n "$arg" ]; then sel=(-k "$arg"); else sel=(); fi
-      timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 160 --timeout-method thread "${sel[@]}" \
+      if [ "$kind" = tests ]; then sel+=(-x); fi
+      timeout -k 10 600 python -u -m pytest tests -m gpu -q -rA --timeout 160 --timeout-method thread "${sel[@]}" \
           >> gpurun_out/$OUT/tests.log 2>&1 ;;
     smoke)
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/$OUT/smoke.log 2>&1 ;;
@@ -49,6 +51,6 @@ for step in "$@"; do
   echo "[gpu_steps] $(date +%T) step $k rc=$rc" | tee -a gpurun_out/$OUT/steps.log
   # failed tests (pytest rc 1) or a script's own assertion (python rc 1) do not
   # end the session; anything else (fault, abort, segfault, time limit) does
-  if [ $rc -ne 0 ] && ! { [ $rc -eq 1 ] && { [ "$kind" = tests ] || [ "$kind" = py ]; }; }; then exit $rc; fi
+  if [ $rc -ne 0 ] && ! { [ $rc -eq 1 ] && { [ "$kind" = tests ] || [ "$kind" = testsall ] || [ "$kind" = py ]; }; }; then exit $rc; fi
 done
 exit 0
