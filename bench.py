@@ -13,11 +13,17 @@ ranks come from the environment.  The conditions are independent, so ranks
 share nothing in the timed region; one RCCL all_gather of the results follows
 it.
 
-  --scaling strong (default)  the fixed BASELINE grid (1024 x 1024) sharded
-                              over the N ranks: rank r solves E_CO rows
-                              r, r+N, ... (every rank samples the whole volcano)
-  --scaling weak              every rank solves its own 1024 x 1024 share of an
-                              (N*1024) x 1024 grid (cyclic rows as above)
+  --scaling weak (default)    every rank solves its own 1024 x 1024 share of an
+                              (N*1024) x 1024 grid: rank r solves E_CO rows
+                              r, r+N, ... (every rank samples the whole volcano);
+                              the per-GPU work is BASELINE configs[2]'s grid at
+                              every N (the task's rule for a path that
+                              partitions into independent units)
+  --scaling strong            the fixed 1024 x 1024 grid sharded over the N
+                              ranks (cyclic rows as above): at N = 8 each GPU
+                              holds 2 048 wavefronts for 3 072 wave slots and
+                              runs at the latency of its slowest wavefronts
+                              (DESIGN.md "Multi-GPU"; tools/emulate_scaling.py)
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--scaling strong|weak]
                     [--config volcano|cstr|dmtm_drc|ch4|synthetic]
@@ -292,6 +298,7 @@ def _solve_workload(wl, sim, net, plan, n, T, p, desc, tof_terms, steady, activi
                         atol=sim.params['atol'] if atol is None else atol, max_steps=args.max_steps,
                         newton=steady and not args.no_newton, newton_iters=30, activity=activity,
                         retry=None if args.no_retry else DEGENERATE_RETRY)
+    wl.solver_launches = 2 if (wl.prm.newton and wl.prm.retry_rtol > 0.0) else 1
     wl.out, wl.o = _outputs(torch, net, n, L, _ptr)
     wl.kf = torch.empty((max(net.NRXN, 1), max(n, 1)), dtype=torch.float64, device='cuda')
     wl.kr = torch.empty_like(wl.kf)
@@ -343,10 +350,13 @@ def volcano_workload(args, rank, world):
     T = float(sim.params['temperature'])
     _solve_workload(wl, sim, net, plan, n, np.full(n, T), None, {'ECO': E1.ravel(), 'EO': E2.ravel()},
                     ('CO_ox',), True, True, args=args)
-    wl.tag = 'volcano %dx%d %s' % (wl.global_grid[0], wl.global_grid[1], args.order)
+    # the profile tag names the per-GPU workload: a weak-scaling rank's share is
+    # the same 1024 x 1024 solve at every N, so N > 1 lines carry its counters
+    wl.tag = 'volcano %dx%d %s' % (rows, G, args.order)
     wl.config = {'workload': 'COOxVolcano %dx%d (E_CO x E_O) grid, %s over %d GPU(s): %d E_CO rows x %d E_O per rank, '
                              'T=600 K, t_end=3600 s, rtol 1e-8 / atol 1e-10, Newton steady-state polish, activity; '
-                             'degenerate roots re-integrated to t_end at rtol %%g / atol %%g in the same launch'
+                             'degenerate roots re-integrated to t_end at rtol %%g / atol %%g (second launch over the '
+                             'compacted list)'
                              % (wl.global_grid[0], wl.global_grid[1], 'sharded' if args.scaling == 'strong'
                                 else 'one grid share per GPU', world, rows, G) % DEGENERATE_RETRY,
                  'global_grid': list(wl.global_grid), 'grid_per_gpu': [rows, G],
@@ -500,7 +510,7 @@ def build_parser():
     ap.add_argument('--steps', type=int, default=10)
     ap.add_argument('--warmup', type=int, default=2)
     ap.add_argument('--config', choices=sorted(CONFIGS), default='volcano')
-    ap.add_argument('--scaling', choices=('strong', 'weak'), default='strong')
+    ap.add_argument('--scaling', choices=('strong', 'weak'), default='weak')
     ap.add_argument('--grid', type=int, default=1024)
     ap.add_argument('--n', type=int, default=0, help='conditions of the non-volcano configs (0: config default)')
     ap.add_argument('--max-steps', type=int, default=200000, help='integrator step budget per condition (library default)')
@@ -520,9 +530,24 @@ def build_parser():
     return ap
 
 
+def _heartbeat(period=45.0):
+    """A line on stderr every `period` s from a daemon thread: one solver
+    launch of a large config (synthetic 1e6) runs for minutes without output,
+    and a GPU-box harness takes a silent process for a hung one."""
+    import threading
+
+    def beat():
+        t0 = time.time()
+        while True:
+            time.sleep(period)
+            log('alive, %.0f s' % (time.time() - t0))
+    threading.Thread(target=beat, daemon=True).start()
+
+
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     args = build_parser().parse_args(argv)
+    _heartbeat()
 
     if 'WORLD_SIZE' not in os.environ and args.gpus > 1:
         if args.emulate:
@@ -623,12 +648,16 @@ def main(argv=None):
         if not cpu:
             fps = flops_per_step(wl.plan)
             fl_struct = fps * steps_local
-            pmc, traffic_src = profiled_counters(wl.kernel_name, wl.tag) if world == 1 else ({}, None)
-            traffic = pmc.get('traffic_bytes')
+            pmc, traffic_src = profiled_counters(wl.kernel_name, wl.tag)
+            # launches of the solver kernel per step: the first pass and, with
+            # the degenerate-root retry, the pass over the compacted list; the
+            # profile's per-launch averages times this are per-step totals
+            nl = getattr(wl, 'solver_launches', 1)
+            traffic = pmc['traffic_bytes'] * nl if 'traffic_bytes' in pmc else None
             # the smaller of the structural count and the fp64 instruction
             # counters of the committed profile of this same workload (which
             # count exec-masked lanes too, so they are an upper bound themselves)
-            fl_pmc = pmc.get('f64_flops_counted')
+            fl_pmc = pmc['f64_flops_counted'] * nl if 'f64_flops_counted' in pmc else None
             fl = min(fl_struct, fl_pmc) if fl_pmc else fl_struct
             achieved = fl / (k3_ms * 1e-3) / 1e12
             roof = {'bound': 'mfma' if False else 'valu_fp64', 'achieved': achieved, 'peak': FP64_VECTOR_PEAK_TFLOPS,
@@ -638,9 +667,10 @@ def main(argv=None):
                     'kernel': wl.kernel_name, 'kernel_ms': k3_ms, 'rate_constants_ms': k1_ms,
                     'flops_per_launch': fl, 'flops_structural': fl_struct, 'flops_pmc_f64': fl_pmc,
                     'flops_per_step': fps, 'flop_count': 'min(structural nonzeros of one accepted Rodas4 step x '
-                    'integrator steps of rank 0 (Newton polish, kernel 1 and TOF not counted), 64 x (ADD+MUL+TRANS) '
-                    '+ 128 x FMA fp64 wave instructions of the committed PMC profile of this workload)',
-                    'integrator_steps': steps_local, 'lane_efficiency': lane_eff}
+                    'integrator steps of rank 0 (both solver launches; Newton polish, kernel 1 and TOF not counted), '
+                    '64 x (ADD+MUL+TRANS) + 128 x FMA fp64 wave instructions of the committed PMC profile of this '
+                    'workload, per launch x solver launches per step)',
+                    'integrator_steps': steps_local, 'lane_efficiency': lane_eff, 'solver_launches_per_step': nl}
             if world == 1 and not args.no_cpu_baseline:
                 avail = host_cores()
                 workers = min(BOX_CPU_SHARE, avail)

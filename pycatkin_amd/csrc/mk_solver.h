@@ -578,17 +578,19 @@ __device__ PCK_LANE_INLINE int integrate(const P& p, const Lane<P::NS>& L, const
     return PCK_ST_OK;
 }
 
-// Is y a root to working precision?  Every species balance that is not a
-// conservation pivot must hold to PCK_BALANCE_TOL of its gross flux
-// (sum over reactions of |S_ij| (r_fwd + r_rev) times the row scale, plus
-// the CSTR flow terms).  Newton's step test holds components below 1e-12 of
-// the largest only to an absolute floor, so on an O-poisoned volcano node it
-// can stop at coverages of 1e-41 that balance nothing (every such equation
-// off by ~100 % of its own flux: the trivial poisoned root approached, TOF ~
-// 1e-36 and undetermined); resolved roots balance to <= 2e-14 (the 2 229
-// regular nodes of tests/golden/volcano_fixture.npz).
+// Is y a root, not an artefact of Newton's absolute floor?  Every species
+// balance that is not a conservation pivot must hold to PCK_BALANCE_TOL of its
+// gross flux (sum over reactions of |S_ij| (r_fwd + r_rev) times the row
+// scale, plus the CSTR flow terms).  Newton's step test holds components below
+// 1e-12 of the largest only to an absolute floor, so on an O-poisoned volcano
+// node it can stop at coverages of 1e-41 that balance nothing (the trivial
+// poisoned root approached, TOF ~1e-36 and undetermined).  Over the 2 560
+// nodes of tests/golden/volcano_fixture.npz the oracle's accepted roots
+// balance either to <= 1e-14 (2 216) or not at all (18, every non-pivot
+// species off by 0.27 to 1 of its flux): the threshold sits in that gap,
+// far from both.
 #ifndef PCK_BALANCE_TOL
-#define PCK_BALANCE_TOL 1e-8
+#define PCK_BALANCE_TOL 1e-3
 #endif
 template <class P, class K>
 __device__ __forceinline__ bool resolved(const P& p, const Lane<P::NS>& L, const K& k, const double (&y)[P::NS]) {

@@ -41,6 +41,14 @@ def test_launcher_world2(scaling, grid):
     assert line['value'] > 0
 
 
+def test_default_multi_gpu_layout_is_weak():
+    """Without --scaling, N ranks each solve a full G x G share: the per-GPU
+    work is BASELINE configs[2]'s grid at every N."""
+    line = _run(['--gpus', '2', '--steps', '1', '--warmup', '0', '--grid', '16'])
+    assert line['scaling'] == 'weak'
+    assert line['config']['global_grid'] == [32, 16] and line['config']['grid_per_gpu'] == [16, 16]
+
+
 def test_launcher_single_rank():
     line = _run(['--steps', '1', '--warmup', '0', '--grid', '16'])
     assert line['n_gpus'] == 1 and line['config']['global_grid'] == [16, 16]
@@ -49,7 +57,7 @@ def test_launcher_single_rank():
 def test_strong_needs_divisible_rows():
     env = {k: v for k, v in os.environ.items() if k not in ('RANK', 'WORLD_SIZE', 'LOCAL_RANK')}
     p = subprocess.run([sys.executable, os.path.join(ROOT, 'bench.py'), '--device', 'cpu-standin', '--gpus', '3',
-                        '--steps', '1', '--warmup', '0', '--grid', '16'], capture_output=True, text=True,
+                        '--steps', '1', '--warmup', '0', '--grid', '16', '--scaling', 'strong'], capture_output=True, text=True,
                        timeout=240, env=env, cwd=ROOT)
     assert p.returncode != 0
 

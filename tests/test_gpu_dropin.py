@@ -94,7 +94,10 @@ def test_volcano_fixture_parity(P, inputs):
     y_t = np.where(fx['tight_ok'][:, None], fx['y_tight'], fx['y_root'])
     assert np.all(fx['tight_ok'][deg] | reg[deg])
     err_tight = rel_l10(l10[deg], l10_t[deg])
-    cov_tight = np.abs(y[deg] - y_t[deg]) <= RTOL * np.abs(y_t[deg]) + 1e-300
+    # coverages: 1e-6 relative above the tight oracle's own absolute accuracy
+    # (its atol 1e-20: a coverage below that is not resolved by the reference
+    # transient either)
+    cov_tight = np.abs(y[deg] - y_t[deg]) <= RTOL * np.abs(y_t[deg]) + 1e-20
     flips = np.nonzero(dev_reg != reg)[0]
     info = dict(n=int(n), n_regular=int(dev_reg.sum()), n_degenerate=int(deg.sum()), n_flips=int(flips.size),
                 flips=[dict(E_CO=float(eco[k]), E_O=float(eo[k]), device_status=int(st[k]),
@@ -112,7 +115,8 @@ def test_volcano_fixture_parity(P, inputs):
     assert np.all(err_root <= RTOL), (err_root.max(), np.nonzero(both)[0][np.argmax(err_root)])
     assert np.all(cov_root)
     assert np.all(err_tight <= RTOL), (err_tight.max(), np.nonzero(deg)[0][np.argmax(err_tight)])
-    assert np.all(cov_tight), np.nonzero(~np.all(cov_tight, axis=1))[0][:10]
+    bad = np.nonzero(~np.all(cov_tight, axis=1))[0]
+    assert bad.size == 0, [(int(np.nonzero(deg)[0][b]), y[deg][b].tolist(), y_t[deg][b].tolist()) for b in bad[:5]]
     # boundary nodes: at most 1 % of the fixture, and each still meets the bound
     # of the semantics it reports (checked above for status 4 against the
     # tight transient; a status-0 flip must be a root of the same equations)

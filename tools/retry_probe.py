@@ -43,7 +43,7 @@ def main():
     o = L.Outputs()
     o.y, o.ld_y, o.tof, o.status, o.nsteps = _ptr(out['y']), n, _ptr(out['tof']), _ptr(out['status']), _ptr(out['nsteps'])
     sp = C.c_void_p(torch.cuda.current_stream().cuda_stream)
-    variants = [None, (1e-8, 1e-22), (1e-9, 1e-21), (1e-10, 1e-20), (1e-7, 1e-22), (1e-12, 1e-24)]
+    variants = [None, (1e-8, 1e-22), (1e-7, 1e-22), (1e-6, 1e-22), (1e-5, 1e-22), (1e-6, 1e-24), (1e-12, 1e-24)]
     res = {}
     inv = np.empty_like(perm)
     inv[perm] = np.arange(n)
