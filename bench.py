@@ -296,7 +296,7 @@ def _solve_workload(wl, sim, net, plan, n, T, p, desc, tof_terms, steady, activi
     wl.prm = net.params(t0=times[0], t_end=times[-1] if t_end is None else t_end,
                         rtol=sim.params['rtol'] if rtol is None else rtol,
                         atol=sim.params['atol'] if atol is None else atol, max_steps=args.max_steps,
-                        newton=steady and not args.no_newton, newton_iters=30, activity=activity,
+                        newton=steady and not args.no_newton, newton_iters=60, activity=activity,
                         retry=None if args.no_retry else DEGENERATE_RETRY)
     wl.solver_launches = 2 if (wl.prm.newton and wl.prm.retry_rtol > 0.0) else 1
     wl.out, wl.o = _outputs(torch, net, n, L, _ptr)
@@ -615,7 +615,8 @@ def main(argv=None):
 
     dev = 'cpu' if cpu else 'cuda'
     st = wl.status()
-    counts = torch.tensor([int((st == 0).sum()), int((st == 4).sum()), int(((st != 0) & (st != 4)).sum()), n],
+    counts = torch.tensor([int((st == 0).sum()), int((st == 4).sum()), int(((st != 0) & (st != 4)).sum()), n,
+                           int((st == 1).sum()), int((st == 2).sum()), int((st == 3).sum())],
                           dtype=torch.int64, device=dev)
     ns = wl.nsteps().double()
     steps_local = float(ns.sum())
@@ -639,7 +640,7 @@ def main(argv=None):
                 E1, E2 = np.meshgrid(np.linspace(-2.5, 0.5, wl.global_grid[0]), np.linspace(-2.5, 0.5, args.grid),
                                      indexing='ij')
                 assert np.allclose(act_map.numpy(), E1 * 10.0 + E2), 'gathered grid out of order'
-    n_ok, n_degen, n_fail, n_total = (int(x) for x in counts.tolist())
+    n_ok, n_degen, n_fail, n_total, n_maxsteps, n_stepfail, n_nonfinite = (int(x) for x in counts.tolist())
     per_step = elapsed / args.steps
     value = n_total / per_step
 
@@ -689,7 +690,8 @@ def main(argv=None):
             'ms_per_step': per_step * 1e3, 'higher_is_better': True, 'scaling': args.scaling, 'vs_baseline': None,
             'dtype': 'f64', 'data': wl.data, 'config': wl.config, 'roofline': roof, 'cpu_baseline': cpu_line,
             'status': {'regular_root': n_ok, 'degenerate_root_tight_transient': n_degen, 'failed': n_fail,
-                       'units': n_total},
+                       'units': n_total, 'failed_by_code': {'max_steps': n_maxsteps, 'step_failure': n_stepfail,
+                                                            'non_finite': n_nonfinite}},
         }
         if args.emulate:
             line['config']['emulated_shard'] = args.emulate

@@ -152,7 +152,7 @@ class SteadyStateSolver:
         s = self.sys
         plan = s.plan()
         y0 = s._to_plan(plan, np.asarray(x0, float)[:, None])
-        r = s.solve_batch(T=[s.T], y0=y0, t0=0.0, t_end=0.0, steady=True, newton_iters=max(int(max_iters), 30))
+        r = s.solve_batch(T=[s.T], y0=y0, t0=0.0, t_end=0.0, steady=True, newton_iters=max(int(max_iters), 60))
         return r['y'][s._from_plan(plan)][:, 0], int(r['status'][0])
 
     def solve_root(self, max_iters=30, method='hybr', use_jac=True, tol=1e-8, test_convergence_kwargs=None,

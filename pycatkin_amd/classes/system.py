@@ -411,7 +411,7 @@ class System:
 
     def solve_batch(self, T=None, p=None, desc=None, y0=None, fix=None, inflow=None, tof_terms=(),
                     steady=False, activity=False, t_end=None, t0=None, rtol=None, atol=None, max_steps=200000,
-                    newton_iters=30, to_numpy=True, t_out=None, retry='auto'):
+                    newton_iters=60, to_numpy=True, t_out=None, retry='auto'):
         """Transient solve to t_end (solve_odes), optionally polished to the
         steady state (find_steady), with TOF or activity per condition; with
         t_out, also the dynamic state at those times ('traj' [n_out, NS, n],
@@ -648,6 +648,6 @@ class System:
         times = self.params.get('times')
         t_end = float(times[-1]) if times is not None and len(times) else 1.0e6
         r = self.solve_batch(T=[self.params['temperature']], y0=np.asarray(yd)[:, None],
-                             t0=0.0, t_end=t_end, steady=True, newton_iters=max(int(max_iters), 30))
+                             t0=0.0, t_end=t_end, steady=True, newton_iters=max(int(max_iters), 60))
         x = np.concatenate([plan.fix_default, r['y'][:, 0]])
         return SteadyStateResults(x, bool(r['status'][0] == 0))

@@ -37,12 +37,6 @@
 namespace pck {
 
 #ifdef PCK_TRACE
-// diagnostic builds only (tools/trace_group.py): per-step records of one condition
-#define PCK_TRACE_N 8192
-#define PCK_TRACE_W 8
-__device__ long long pck_trace_cond = -1;
-__device__ int pck_trace_pos = 0;
-__device__ double pck_trace_buf[PCK_TRACE_N * PCK_TRACE_W];
 // shader-clock cycles of the traced condition's integrator phases:
 // [jac, lu, solve, rhs, other, steps]
 __device__ double pck_phase[8];
@@ -803,11 +797,12 @@ __device__ __forceinline__ double rec_gross(const uint4& rec, double a, double b
     return fabs(a) + fabs(b);
 }
 
-// mk_solver.h: resolved -- every non-pivot species balance within
-// PCK_BALANCE_TOL of its gross flux (group-uniform result)
+// mk_solver.h: imbalance -- the largest |f_i| / gross_i over the rows that are
+// not conservation pivots (group-uniform); f = the row's rate (grp_rhs)
 template <int NSP, int G>
-__device__ __forceinline__ bool grp_resolved(const NetView& nv, const GrpView& g, const Grp<NSP>& x, double y) {
-    const double f = grp_rhs<NSP, G>(g, x, y);
+__device__ __forceinline__ double grp_imbalance(const NetView& nv, const GrpView& g, const Grp<NSP>& x, double y,
+                                                double& f) {
+    f = grp_rhs<NSP, G>(g, x, y);
     wsync();                                   // the rows' reads of the net rates are done
     for (int r = x.gl; r < x.R; r += G) x.d[r] = rec_gross(g.rx[r], x.kf[r], x.kr[r], x.c);
     wsync();
@@ -821,8 +816,13 @@ __device__ __forceinline__ bool grp_resolved(const NetView& nv, const GrpView& g
     }
     bool pv = false;
     for (int l = 0; l < nv.NCONS; ++l) pv = pv || (nv.cpiv[l] == x.gl);
-    const bool bad = x.row && !pv && !(fabs(f) <= PCK_BALANCE_TOL * gr);
-    return gmaxi<G>(bad ? 1 : 0) == 0;
+    return gmax<G>((x.row && !pv && f != 0.0) ? fabs(f) / gr : 0.0);
+}
+
+template <int NSP, int G>
+__device__ __forceinline__ bool grp_resolved(const NetView& nv, const GrpView& g, const Grp<NSP>& x, double y) {
+    double f;
+    return grp_imbalance<NSP, G>(nv, g, x, y, f) <= PCK_BALANCE_TOL;
 }
 
 // Newton steady-state polish (same rules as mk_solver.h: newton)
@@ -840,12 +840,17 @@ __device__ __forceinline__ int grp_newton(const NetView& nv, const GrpView& gv, 
             piv_l[l] = nv.cpiv[l];
         }
     }
-    double z = y;
+    double z = y, z_prev = y, bal_prev = INFINITY;
     bool conv = false;
     double prev = INFINITY, lastq = 1.0;
     int linear = 0;
     for (int it = 0; it < iters; ++it) {
-        double Gv = grp_rhs<NSP, G>(gv, x, z);
+        double Gv;
+        // the rounding floor (mk_solver.h: PCK_BALANCE_CONV)
+        const double bal = grp_imbalance<NSP, G>(nv, gv, x, z, Gv);
+        if (it >= 2 && bal_prev <= PCK_BALANCE_CONV && bal > bal_prev) { z = z_prev; conv = true; break; }
+        bal_prev = bal;
+        z_prev = z;
         grp_jac<NSP, G, P>(nv, gv, x, z, 1.0, 0.0, F.W);
 #pragma unroll
         for (int l = 0; l < PCK_MAX_CONS; ++l) {

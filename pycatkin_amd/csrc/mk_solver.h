@@ -18,6 +18,16 @@
 
 namespace pck {
 
+#ifdef PCK_TRACE
+// diagnostic builds only (tools/trace_group.py, tools/trace_newton.py):
+// records of one condition (lane-group integrator steps, lane Newton iterations)
+#define PCK_TRACE_N 8192
+#define PCK_TRACE_W 8
+__device__ long long pck_trace_cond = -1;
+__device__ int pck_trace_pos = 0;
+__device__ double pck_trace_buf[PCK_TRACE_N * PCK_TRACE_W];
+#endif
+
 template <int NS_>
 struct PlanRT {
     static constexpr int NS = NS_;
@@ -91,6 +101,9 @@ struct Lane {
     double T;
     const double* ins;   // this lane's inflow column in LDS (stride ks), flow rows only
     int ks;
+#ifdef PCK_TRACE
+    int64_t cidx;        // condition index (trace builds)
+#endif
 };
 
 // ---------------------------------------------------------------------------
@@ -191,6 +204,9 @@ __device__ __forceinline__ void lane_setup(const P& p, const NetView& nv, const 
                                            Lane<P::NS>& L, double* lds_lane, int ks) {
     L.T = cv.T[c * cv.sT];           // reactor.py:34-41: CSTR row scaling is linear in T
     L.ks = ks;
+#ifdef PCK_TRACE
+    L.cidx = c;
+#endif
     double* ins = lds_lane + (size_t)2 * nv.NRXN * ks;
     L.ins = ins;
 #pragma unroll
@@ -593,9 +609,10 @@ __device__ PCK_LANE_INLINE int integrate(const P& p, const Lane<P::NS>& L, const
 #define PCK_BALANCE_TOL 1e-3
 #endif
 template <class P, class K>
-__device__ __forceinline__ bool resolved(const P& p, const Lane<P::NS>& L, const K& k, const double (&y)[P::NS]) {
+__device__ __forceinline__ void rhs_gross(const P& p, const Lane<P::NS>& L, const K& k, const double (&y)[P::NS],
+                                          double (&f)[P::NS], double (&g)[P::NS]) {
     constexpr int NS = P::NS;
-    double c[NS], f[NS], g[NS];
+    double c[NS];
 #pragma unroll
     for (int i = 0; i < NS; ++i) { c[i] = p.cf(i) * y[i]; f[i] = 0.0; g[i] = 0.0; }
     for_rxn(p, [&](int j) {
@@ -612,7 +629,6 @@ __device__ __forceinline__ bool resolved(const P& p, const Lane<P::NS>& L, const
             if (s != 0.0) { f[i] += s * net; g[i] += fabs(s) * gross; }
         }
     });
-    bool ok = true;
 #pragma unroll
     for (int i = 0; i < NS; ++i) {
         const double rs = (p.rsT(i) != 0.0) ? p.rs0(i) + p.rsT(i) * L.T : p.rs0(i);
@@ -622,12 +638,54 @@ __device__ __forceinline__ bool resolved(const P& p, const Lane<P::NS>& L, const
             f[i] += p.fl(i) * (L.ins[i * L.ks] - y[i]);
             g[i] += fabs(p.fl(i)) * (fabs(L.ins[i * L.ks]) + fabs(y[i]));
         }
+    }
+}
+
+// every species balance except the conservation pivots within tol of its gross flux
+template <class P>
+__device__ __forceinline__ bool balanced(const P& p, const double (&f)[P::NS], const double (&g)[P::NS], double tol) {
+    bool ok = true;
+#pragma unroll
+    for (int i = 0; i < P::NS; ++i) {
         bool pv = false;
         for (int l = 0; l < p.ncons(); ++l) pv = pv || (p.cpiv(l) == i);
-        ok = ok && (pv || fabs(f[i]) <= PCK_BALANCE_TOL * g[i]);
+        ok = ok && (pv || fabs(f[i]) <= tol * g[i]);
     }
     return ok;
 }
+
+// the largest |f_i| / gross_i over the species that are not conservation pivots
+template <class P>
+__device__ __forceinline__ double imbalance(const P& p, const double (&f)[P::NS], const double (&g)[P::NS]) {
+    double m = 0.0;
+#pragma unroll
+    for (int i = 0; i < P::NS; ++i) {
+        bool pv = false;
+        for (int l = 0; l < p.ncons(); ++l) pv = pv || (p.cpiv(l) == i);
+        if (!pv && f[i] != 0.0) m = fmax(m, fabs(f[i]) / g[i]);
+    }
+    return m;
+}
+
+template <class P, class K>
+__device__ __forceinline__ bool resolved(const P& p, const Lane<P::NS>& L, const K& k, const double (&y)[P::NS]) {
+    double f[P::NS], g[P::NS];
+    rhs_gross(p, L, k, y, f, g);
+    return balanced(p, f, g, PCK_BALANCE_TOL);
+}
+
+// Newton's stop at the rounding floor: once a Newton iterate balances every
+// species to PCK_BALANCE_CONV of its gross flux, a next step that makes the
+// balance worse is rounding noise amplified by the Jacobian's condition (up
+// to 1e12 at a site-starved volcano root), not progress: the iteration keeps
+// the better point and stops.  On fixture node 80 the device took such a
+// step from the root, landed 10 % away on the 2.8e-10 free-site coverage and
+// came back in a 12-iteration cycle until the iteration cap
+// (tools/trace_newton.py), while LAPACK's solve in the oracle happened to
+// land on the root.
+#ifndef PCK_BALANCE_CONV
+#define PCK_BALANCE_CONV 1e-10
+#endif
 
 // Newton on f(y) = 0 with the plan's conservation laws replacing their pivot
 // rows (old_system.py:385-468 polishes with scipy least_squares; a regular
@@ -645,16 +703,30 @@ __device__ PCK_LANE_INLINE int newton(const P& p, const Lane<P::NS>& L, const K&
         for (int i = 0; i < NS; ++i) s += p.C(l, i) * y[i];
         b[l] = s;
     }
-    double z[NS];
+    double z[NS], z_prev[NS];
 #pragma unroll
     for (int i = 0; i < NS; ++i) z[i] = y[i];
+    double bal_prev = INFINITY;
     bool conv = false;
     double prev = INFINITY, lastq = 1.0;
     int linear = 0;
     for (int it = 0; it < iters; ++it) {
         double G[NS], J[NS][NS];
         int piv[NS];
-        rhs(p, L, k, z, G);
+        {
+            double Gg[NS];
+            rhs_gross(p, L, k, z, G, Gg);
+            const double bal = imbalance(p, G, Gg);
+            if (it >= 2 && bal_prev <= PCK_BALANCE_CONV && bal > bal_prev) {   // the rounding floor
+#pragma unroll
+                for (int i = 0; i < NS; ++i) z[i] = z_prev[i];
+                conv = true;
+                break;
+            }
+            bal_prev = bal;
+#pragma unroll
+            for (int i = 0; i < NS; ++i) z_prev[i] = z[i];
+        }
         jac(p, L, k, z, J);
         for (int l = 0; l < p.ncons(); ++l) {
             const int pv = p.cpiv(l);
@@ -684,7 +756,7 @@ __device__ PCK_LANE_INLINE int newton(const P& p, const Lane<P::NS>& L, const K&
             G[i] = -G[i] * sc;
         }
         unsigned sw;
-        if (!lu<NS>(J, piv, sw)) break;
+        if (!lu<NS, true>(J, piv, sw)) break;
         lu_solve<NS>(J, piv, sw, G);
         double alpha = 1.0;
         if (linear >= 2 && lastq < 0.9) {
@@ -708,12 +780,31 @@ __device__ PCK_LANE_INLINE int newton(const P& p, const Lane<P::NS>& L, const K&
         // 1e-24 * zmax: their relative digits sit under the residual's rounding
 #pragma unroll
         for (int i = 0; i < NS; ++i) rel = fmax(rel, fabs(G[i]) / fmax(fabs(z[i]), 1e-12 * zmax + 1e-300));
+#ifdef PCK_TRACE
+        if (L.cidx == pck_trace_cond) {           // [it, rel, alpha, z0..z4]
+            double* rec = pck_trace_buf + (size_t)(pck_trace_pos % PCK_TRACE_N) * PCK_TRACE_W;
+            rec[0] = it; rec[1] = rel; rec[2] = alpha;
+#pragma unroll
+            for (int i = 0; i < NS && i < PCK_TRACE_W - 3; ++i) rec[3 + i] = z[i];
+            pck_trace_pos = pck_trace_pos + 1;
+        }
+#endif
         if (rel < 1e-12 || (it >= 2 && rel < 1e-7 && rel > 0.5 * prev)) { conv = true; break; }
         lastq = rel / prev;
         linear = (rel > 0.25 * prev) ? linear + 1 : 0;
         if (linear >= 12) break;
         prev = rel;
     }
+#ifdef PCK_TRACE
+    if (L.cidx == pck_trace_cond) {               // exit record: [-1, conv, min z, resolved]
+        double* rec = pck_trace_buf + (size_t)(pck_trace_pos % PCK_TRACE_N) * PCK_TRACE_W;
+        double zmin = z[0];
+#pragma unroll
+        for (int i = 1; i < NS; ++i) zmin = fmin(zmin, z[i]);
+        rec[0] = -1.0; rec[1] = conv ? 1.0 : 0.0; rec[2] = zmin; rec[3] = resolved(p, L, k, z) ? 1.0 : 0.0;
+        pck_trace_pos = pck_trace_pos + 1;
+    }
+#endif
     if (!conv) return PCK_ST_NEWTON;
 #pragma unroll
     for (int i = 0; i < NS; ++i)

@@ -169,7 +169,7 @@ class DeviceNetwork:
         return out.reshape(self.NDYN, self.NDYN, n)
 
     @staticmethod
-    def params(t_end, t0=0.0, rtol=1e-8, atol=1e-10, max_steps=100000, newton=False, newton_iters=30,
+    def params(t_end, t0=0.0, rtol=1e-8, atol=1e-10, max_steps=100000, newton=False, newton_iters=60,
                activity=False, drc_eps=1e-3, retry=None):
         """retry = (rtol, atol): with newton, the conditions whose polish meets a
         degenerate root (status 4) are integrated again at these tolerances

@@ -62,7 +62,7 @@ def run(sim, T, desc, tof_terms, steady, drc, reps, torch, t_end=None, rtol=None
     times = sim.params['times']
     prm = net.params(t0=times[0], t_end=times[-1] if t_end is None else t_end,
                      rtol=sim.params['rtol'] if rtol is None else rtol, atol=sim.params['atol'] if atol is None else atol,
-                     max_steps=max_steps, newton=steady, newton_iters=30, drc_eps=eps)
+                     max_steps=max_steps, newton=steady, newton_iters=60, drc_eps=eps)
     sp = C.c_void_p(torch.cuda.current_stream().cuda_stream)
     st = torch.zeros(n, dtype=torch.int32, device='cuda')
     if drc:
