@@ -26,6 +26,7 @@ def main():
     ap.add_argument('--max-steps', type=int, default=200000)
     ap.add_argument('--no-newton', action='store_true')
     ap.add_argument('--runtime-plan', action='store_true')
+    ap.add_argument('--no-retry', action='store_true')
     a = ap.parse_args(sys.argv[2:])
     torch.cuda.set_device(0)
     wl = bench.volcano_workload(a, 0, 1)
@@ -35,6 +36,7 @@ def main():
     os.makedirs(os.path.join(ROOT, 'gpurun_out'), exist_ok=True)
     np.save(os.path.join(ROOT, 'gpurun_out', out + '.npy'), wl.nsteps().cpu().numpy())
     np.save(os.path.join(ROOT, 'gpurun_out', out + '_status.npy'), wl.status().cpu().numpy())
+    np.save(os.path.join(ROOT, 'gpurun_out', out + '_perm.npy'), wl.perm if wl.perm is not None else np.arange(wl.n_local))
     print('saved', out, int(wl.nsteps().sum()))
 
 

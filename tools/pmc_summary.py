@@ -50,8 +50,16 @@ def summarise(d):
 
 
 if __name__ == '__main__':
+    # python tools/pmc_summary.py DIR [--tag KERNEL_SUBSTRING TAG]: the tag names
+    # the bench workload the profile is of (bench.py: profiled_counters)
     d = sys.argv[1]
     s = summarise(d)
+    if '--tag' in sys.argv:
+        i = sys.argv.index('--tag')
+        sub, tag = sys.argv[i + 1], sys.argv[i + 2]
+        for k, v in s.items():
+            if sub in k:
+                v['tag'] = tag
     with open(os.path.join(d, 'summary.json'), 'w') as fh:
         json.dump(s, fh, indent=1, sort_keys=True)
     for k, v in s.items():
