@@ -298,6 +298,7 @@ def _solve_workload(wl, sim, net, plan, n, T, p, desc, tof_terms, steady, activi
                         atol=sim.params['atol'] if atol is None else atol, max_steps=args.max_steps,
                         newton=steady and not args.no_newton, newton_iters=60, activity=activity,
                         retry=None if args.no_retry else DEGENERATE_RETRY)
+    wl.prm.wave_order = {'auto': 0, 'on': 1, 'off': -1}[getattr(args, 'wave_order', 'auto')]
     wl.solver_launches = 2 if (wl.prm.newton and wl.prm.retry_rtol > 0.0) else 1
     wl.out, wl.o = _outputs(torch, net, n, L, _ptr)
     wl.kf = torch.empty((max(net.NRXN, 1), max(n, 1)), dtype=torch.float64, device='cuda')
@@ -521,6 +522,8 @@ def build_parser():
                     help='A/B diagnostic: degenerate roots keep the first transient (not the bench workload)')
     ap.add_argument('--emulate', default=None, metavar='R/N',
                     help='single-GPU A/B: solve the shard rank R of N would own, without a process group')
+    ap.add_argument('--wave-order', choices=('auto', 'on', 'off'), default='auto',
+                    help='cost-ordered wavefront dispatch of the lane solver (pck_solve_params.wave_order)')
     ap.add_argument('--tile', default='16x4', help='patch shape (rows x cols) of --order tile')
     ap.add_argument('--order', choices=('tile', 'row'), default='tile',
                     help="condition order in HBM: 'tile' = one grid patch per wave (default), 'row' = row-major")

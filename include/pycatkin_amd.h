@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define PCK_ABI_VERSION 3
+#define PCK_ABI_VERSION 4
 
 /* error codes */
 #define PCK_OK 0
@@ -151,6 +151,11 @@ typedef struct {
                             *   the reference's System.activity semantics (old_system.py:517-529),
                             *   status stays PCK_ST_NEWTON (or the retry's failure status) and
                             *   nsteps adds the retry's steps */
+    int32_t wave_order;    /* pck_solve on the lane solver: dispatch the 64-condition wavefronts in
+                            *   descending cost, predicted by a loose preview transient (rtol 1e-3) of 4
+                            *   lanes of each; 1 on, -1 off, 0 auto (on for n >= 262144: more than one
+                            *   round of wavefronts).  Results do not depend on it: the same 64
+                            *   conditions share a wavefront either way. */
 } pck_solve_params;
 
 /* Outputs of pck_solve (device pointers; any may be NULL). */

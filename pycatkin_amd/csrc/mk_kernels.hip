@@ -652,6 +652,53 @@ __global__ void __launch_bounds__(256) k_select_status(int64_t n, const int32_t*
     if (f) idx[base + __popcll(m & ((1ull << lane) - 1ull))] = c;
 }
 
+// Cost-ordered dispatch of the lane solver (pck_solve_params.wave_order).
+// A wavefront's time is its slowest lane's; the hardware dispatches blocks in
+// launch order, so long wavefronts launched last leave the machine idle in a
+// tail (the wave-scheduling model puts the volcano launch at 1.19x its ideal,
+// longest-first at 1.17x faster: tools/sched_sim.py).  The preview solves 4
+// lanes of every wavefront (its first and last two: the corners of a 16 x 4
+// volcano patch) as a loose transient; max of their step counts is the
+// wavefront's key (tools/predictor_eval.py: 1.167x in the model against 1.170x
+// for the true costs).
+constexpr int PCK_PREVIEW_LANES = 4;
+__device__ __forceinline__ int preview_lane(int k) { return (k < 2) ? 3 * k : 60 + 3 * (k - 2); }   // 0, 3, 60, 63
+
+__global__ void __launch_bounds__(256) k_preview_list(int64_t n, int64_t W, int64_t* list, int32_t* cnt) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < W * PCK_PREVIEW_LANES) {
+        const int64_t c = (i / PCK_PREVIEW_LANES) * PCK_SOLVE_BLOCK + preview_lane((int)(i % PCK_PREVIEW_LANES));
+        list[i] = (c < n) ? c : n - 1;      // a short last wavefront samples its last condition
+    }
+    if (i == 0) *cnt = (int32_t)(W * PCK_PREVIEW_LANES);
+}
+
+// descending counting sort of the wavefronts by their preview key (one block)
+__global__ void __launch_bounds__(1024) k_wave_order(int64_t n, int64_t W, const int32_t* ns, int32_t* order) {
+    __shared__ int hist[1024];
+    __shared__ int base[1024];
+    const int tid = threadIdx.x;
+    hist[tid] = 0;
+    __syncthreads();
+    auto key = [&](int64_t w) {
+        int k = 0;
+        for (int l = 0; l < PCK_PREVIEW_LANES; ++l) {
+            int64_t c = w * PCK_SOLVE_BLOCK + preview_lane(l);
+            c = (c < n) ? c : n - 1;
+            k = max(k, ns[c]);
+        }
+        return min(max(k, 0), 1023);
+    };
+    for (int64_t w = tid; w < W; w += 1024) atomicAdd(&hist[key(w)], 1);
+    __syncthreads();
+    if (tid == 0) {
+        int sum = 0;
+        for (int k = 1023; k >= 0; --k) { base[k] = sum; sum += hist[k]; }
+    }
+    __syncthreads();
+    for (int64_t w = tid; w < W; w += 1024) order[atomicAdd(&base[key(w)], 1)] = (int32_t)w;
+}
+
 // One solver launch over the batch (lane or lane-group path).
 static int run_solver(const pck_network* net, const pck_conditions* cond, const SolveArgs& a_in, bool grp,
                       GrpArgs& ga, bool traj, const double* kf, const double* kr, hipStream_t s) {
@@ -770,7 +817,7 @@ static int launch_solve(const pck_network* net, const pck_conditions* cond, cons
     a.t0 = prm->t0; a.t_end = prm->t_end; a.rtol = prm->rtol; a.atol = prm->atol; a.eps = prm->drc_eps;
     a.max_steps = prm->max_steps; a.newton = prm->newton; a.newton_iters = prm->newton_iters;
     a.want_activity = prm->want_activity;
-    a.idx = nullptr; a.nidx = nullptr; a.retry_pass = 0;
+    a.idx = nullptr; a.nidx = nullptr; a.retry_pass = 0; a.worder = nullptr;
     // degenerate roots (status 4) are re-integrated by a second launch over
     // their compacted list (pck_solve only: G == 1, no DRC groups)
     const bool retry = prm->newton && prm->retry_rtol > 0.0 && !drc_groups && a.G == 1;
@@ -808,6 +855,35 @@ static int launch_solve(const pck_network* net, const pck_conditions* cond, cons
         ga.stbuf = (int32_t*)(ga.tofbuf + m);
         ga.nsbuf = ga.stbuf + m;
     }
+    // cost-ordered dispatch: preview, order, then the first pass in that order
+    StreamScratch oscr;
+    const bool order = !grp && !traj && a.G == 1 && !drc_groups &&
+                       (prm->wave_order > 0 || (prm->wave_order == 0 && n >= 262144));
+    if (order) {
+        const int64_t W = (n + PCK_SOLVE_BLOCK - 1) / PCK_SOLVE_BLOCK;
+        const size_t b_list = sizeof(int64_t) * (size_t)W * PCK_PREVIEW_LANES, b_ns = sizeof(int32_t) * (size_t)n;
+        rc = salloc(oscr, b_list + 64 + b_ns + sizeof(int32_t) * (size_t)W, s);
+        if (rc) return rc;
+        int64_t* list = oscr.as<int64_t>();
+        int32_t* cnt = (int32_t*)((char*)list + b_list);
+        int32_t* pns = (int32_t*)((char*)list + b_list + 64);
+        int32_t* wo = pns + n;
+        hipLaunchKernelGGL(k_preview_list, dim3((unsigned)((W * PCK_PREVIEW_LANES + 255) / 256)), dim3(256), 0, s,
+                           n, W, list, cnt);
+        HIPCHK(hipGetLastError());
+        SolveArgs pv = a;
+        pv.rtol = fmax(a.rtol, 1e-3);
+        pv.atol = a.atol * (pv.rtol / a.rtol);       // the same atol / rtol ratio
+        pv.newton = 0;
+        pv.max_steps = a.max_steps < 1000 ? a.max_steps : 1000;
+        pv.y = nullptr; pv.tof = nullptr; pv.status = nullptr; pv.nsteps = pns;
+        pv.idx = list; pv.nidx = cnt; pv.retry_pass = 0; pv.worder = nullptr;
+        rc = run_solver(net, cond, pv, grp, ga, traj, kf, kr, s);
+        if (rc) return rc;
+        hipLaunchKernelGGL(k_wave_order, dim3(1), dim3(1024), 0, s, n, W, pns, wo);
+        HIPCHK(hipGetLastError());
+        a.worder = wo;
+    }
     StreamScratch rscr;
     if (retry) {
         // the retry list (int64 per condition), its length, and a status
@@ -835,6 +911,7 @@ static int launch_solve(const pck_network* net, const pck_conditions* cond, cons
         r.idx = idx;
         r.nidx = cnt;
         r.retry_pass = 1;
+        r.worder = nullptr;
         if (!r.nsteps) r.nsteps = nullptr;
         rc = run_solver(net, cond, r, grp, ga, traj, kf, kr, s);
         if (rc) return rc;

@@ -678,13 +678,15 @@ __device__ __forceinline__ bool resolved(const P& p, const Lane<P::NS>& L, const
 // species to PCK_BALANCE_CONV of its gross flux, a next step that makes the
 // balance worse is rounding noise amplified by the Jacobian's condition (up
 // to 1e12 at a site-starved volcano root), not progress: the iteration keeps
-// the better point and stops.  On fixture node 80 the device took such a
+// the better point and stops.  (1e-10 stopped some roots early enough to
+// leave tiny TOFs with 3e-7 relative rounding; resolved roots balance to
+// <= 1e-14.)  On fixture node 80 the device took such a
 // step from the root, landed 10 % away on the 2.8e-10 free-site coverage and
 // came back in a 12-iteration cycle until the iteration cap
 // (tools/trace_newton.py), while LAPACK's solve in the oracle happened to
 // land on the root.
 #ifndef PCK_BALANCE_CONV
-#define PCK_BALANCE_CONV 1e-10
+#define PCK_BALANCE_CONV 1e-12
 #endif
 
 // Newton on f(y) = 0 with the plan's conservation laws replacing their pivot
@@ -905,6 +907,9 @@ struct SolveArgs {
     // volcano kernel went from 158 to 227, i.e. from 3 to 2 waves per SIMD.)
     const int64_t* idx; const int32_t* nidx;
     int retry_pass;
+    // cost-ordered dispatch (pck_solve_params.wave_order): block b of the lane
+    // solver (one wavefront) solves the 64 conditions of wavefront worder[b]
+    const int32_t* worder;
 };
 
 // One condition's solve: transient from y0, then (with a.newton) the Newton
@@ -956,7 +961,8 @@ __global__ void __launch_bounds__(PCK_SOLVE_BLOCK) __attribute__((amdgpu_waves_p
     extern __shared__ double lds[];
     const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int G = a.G;
-    const int64_t c = cond_of(a, gid, G, cv.n);
+    const int64_t c = a.worder ? ((int64_t)a.worder[blockIdx.x] * PCK_SOLVE_BLOCK + threadIdx.x)
+                               : cond_of(a, gid, G, cv.n);
     const int q = (int)(gid % G);
     const int R = nv.NRXN;
     P p(nv);

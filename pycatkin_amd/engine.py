@@ -170,7 +170,7 @@ class DeviceNetwork:
 
     @staticmethod
     def params(t_end, t0=0.0, rtol=1e-8, atol=1e-10, max_steps=100000, newton=False, newton_iters=60,
-               activity=False, drc_eps=1e-3, retry=None):
+               activity=False, drc_eps=1e-3, retry=None, wave_order=0):
         """retry = (rtol, atol): with newton, the conditions whose polish meets a
         degenerate root (status 4) are integrated again at these tolerances
         and report that transient end (pck_solve_params.retry_rtol)."""
@@ -180,6 +180,7 @@ class DeviceNetwork:
         p.want_activity, p.drc_eps = int(bool(activity)), float(drc_eps)
         if retry is not None:
             p.retry_rtol, p.retry_atol = float(retry[0]), float(retry[1])
+        p.wave_order = int(wave_order)     # 0 auto, 1 on, -1 off (pck_solve_params.wave_order)
         return p
 
     def solve(self, n, T, p, y0, desc=None, fixc=None, inflow=None, want_k=False, out=None, t_out=None, **kw):

@@ -354,7 +354,10 @@ def test_jit_plan_matches_runtime_plan(P, inputs):
     assert np.mean(both) > 0.9, (np.unique(a['status'], return_counts=True), np.unique(b['status'], return_counts=True))
     assert np.mean(a['status'] != b['status']) < 0.05
     assert close_cov(a['y'][:, both], b['y'][:, both], rtol=1e-7, floor=1e-14), np.abs(a['y'] - b['y'])[:, both].max()
-    np.testing.assert_allclose(a['tof'][both], b['tof'][both], rtol=1e-7)
+    # TOF at north_star's 1e-6: the two compilations round differently, and a
+    # root met at Newton's linear exit (rel < 1e-7) carries that into a tiny
+    # TOF (one of these 463 regular roots: 2.3e-20, 3.1e-7 apart)
+    np.testing.assert_allclose(a['tof'][both], b['tof'][both], rtol=1e-6)
 
 
 def test_jit_can_be_disabled(P, inputs, monkeypatch):
@@ -564,3 +567,46 @@ def test_two_streams_share_one_network(P, inputs):
     for r, ref in ((r1, ref1), (r2, ref2)):
         for key in ('y', 'tof', 'status'):
             np.testing.assert_array_equal(r[key].cpu().numpy(), ref[key])
+
+
+def test_wave_order_does_not_change_results(P, inputs):
+    """Cost-ordered dispatch (pck_solve_params.wave_order: a loose preview of
+    4 lanes per wavefront, then the wavefronts longest-first) only changes
+    WHEN each 64-condition wavefront runs, not which conditions share it:
+    every output is bitwise equal to the launch-order solve (512 x 512 grid in
+    16 x 4 patch order, Newton and the degenerate-root retry included)."""
+    import torch
+    from pycatkin_amd.functions.volcano import set_volcano_energies, tile_order
+    from pycatkin_amd import _lib as L
+    import ctypes as C
+    from pycatkin_amd.engine import _ptr
+    s = P.read_from_input_file(os.path.join(inputs, 'COOxVolcano', 'input.json'))
+    set_volcano_energies(s)
+    plan = s.plan(('CO_ox',))
+    net = s.device(('CO_ox',))
+    G = 512
+    be = np.linspace(-2.5, 0.5, G)
+    E1, E2 = np.meshgrid(be, be, indexing='ij')
+    perm = tile_order(E1.shape)
+    n = E1.size
+    T, p, d, fx, y0, inflow = s._inputs(net, plan, n, np.full(n, 600.0), None,
+                                        {'ECO': E1.ravel()[perm], 'EO': E2.ravel()[perm]}, None, None, None)
+    cond, keep = net.conditions(n, T, p, d, fx, y0, inflow)
+    from pycatkin_amd.classes.system import DEGENERATE_RETRY
+    res = {}
+    for mode in (-1, 1):
+        out = dict(y=torch.empty((net.NDYN, n), dtype=torch.float64, device='cuda'),
+                   tof=torch.empty(n, dtype=torch.float64, device='cuda'),
+                   status=torch.empty(n, dtype=torch.int32, device='cuda'),
+                   nsteps=torch.empty(n, dtype=torch.int32, device='cuda'))
+        o = L.Outputs()
+        o.y, o.ld_y, o.tof, o.status, o.nsteps = _ptr(out['y']), n, _ptr(out['tof']), _ptr(out['status']), \
+            _ptr(out['nsteps'])
+        prm = net.params(t0=0.0, t_end=3600.0, rtol=1e-8, atol=1e-10, max_steps=200000, newton=True,
+                         retry=DEGENERATE_RETRY, wave_order=mode)
+        L.check(net.lib.pck_solve(net.h, C.byref(cond), C.byref(prm), C.byref(o),
+                                  C.c_void_p(torch.cuda.current_stream().cuda_stream)))
+        res[mode] = {k: v.cpu().numpy() for k, v in out.items()}
+    for k in ('y', 'tof', 'status', 'nsteps'):
+        np.testing.assert_array_equal(res[1][k], res[-1][k])
+    assert np.mean(res[1]['status'] == 0) > 0.8
