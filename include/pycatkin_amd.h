@@ -149,8 +149,8 @@ typedef struct {
                             *   the same stream (pck_solve only; 0: off); its y / tof become that
                             *   transient end,
                             *   the reference's System.activity semantics (old_system.py:517-529),
-                            *   status stays PCK_ST_NEWTON (or the retry's failure status) and
-                            *   nsteps adds the retry's steps */
+                            *   status stays PCK_ST_NEWTON and nsteps adds the retry's steps; a
+                            *   retry that fails keeps the first pass's y / tof (PCK_ST_NEWTON_LOOSE) */
     int32_t wave_order;    /* pck_solve on the lane solver: dispatch the 64-condition wavefronts in
                             *   descending cost, predicted by a loose preview transient (rtol 1e-3) of 4
                             *   lanes of each; 1 on, -1 off, 0 auto (on for n >= 262144: more than one
@@ -177,6 +177,10 @@ typedef struct {
 #define PCK_ST_STEPFAIL 2
 #define PCK_ST_NONFINITE 3
 #define PCK_ST_NEWTON 4
+/* a degenerate root whose tight retry transient failed (step budget / step
+ * size): y and tof are the first pass's transient end at the caller's
+ * tolerances -- what the reference's own lsoda path reports */
+#define PCK_ST_NEWTON_LOOSE 5
 
 int pck_abi_version(void);
 const char* pck_last_error(void);

@@ -583,11 +583,13 @@ class System:
     @staticmethod
     def _check(st, what, degenerate_ok=False):
         """Raise on a failed solve (1 max steps, 2 step failure, 3 non-finite);
-        status 4 (degenerate root, transient end reported) is a result where
-        the reference's steady-state path would return one."""
-        if st != 0 and not (degenerate_ok and st == 4):
+        status 4 (degenerate root, tight transient end reported) and 5 (its
+        tight retry failed: the first pass's transient at the caller's
+        tolerances) are results where the reference's steady-state path
+        would return one."""
+        if st != 0 and not (degenerate_ok and st in (4, 5)):
             raise RuntimeError('%s: device solver status %d (1 max steps, 2 step failure, 3 non-finite, '
-                               '4 Newton failure)' % (what, st))
+                               '4 degenerate root, 5 degenerate root with the first-pass transient)' % (what, st))
 
     def reaction_terms(self, y):
         """old_system.py:202-225: rates (n_reactions, 2) at the full state y."""

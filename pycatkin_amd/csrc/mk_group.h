@@ -1021,7 +1021,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 64
     int st = grp_integrate<NSP, G, P, TRAJ>(nv, gl, x, y, a.t0, a.t_end, a.rtol, a.atol, a.max_steps, ns,
                                             a.cons_rows != 0, to, F);
     if (st == PCK_ST_OK && a.newton) st = grp_newton<NSP, G, P>(nv, gl, x, y, a.newton_iters, F);
-    if (a.retry_pass && st == PCK_ST_OK) st = PCK_ST_NEWTON;
     const double tof = grp_tof<NSP, G>(nv, gl, x, y);
     const bool fin = gmin<G>((!x.row || isfinite(y)) ? 1.0 : 0.0) > 0.0 && isfinite(tof);
     if (!fin && st == PCK_ST_OK) st = PCK_ST_NONFINITE;
@@ -1033,9 +1032,14 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 64
         }
         return;
     }
-    if (a.y && x.row) a.y[x.gl * a.ld_y + c] = y;
+    // retry pass (mk_solver.h: k_solve): a failed tight transient keeps the
+    // first pass's outputs
+    const bool keep = a.retry_pass && st != PCK_ST_OK;
+    if (a.retry_pass) st = keep ? PCK_ST_NEWTON_LOOSE : PCK_ST_NEWTON;
+    if (a.y && x.row && !keep) a.y[x.gl * a.ld_y + c] = y;
     if (x.gl == 0) {
-        if (a.tof) a.tof[c] = a.want_activity ? (log((hP * tof) / (kB * T)) * (Rgas * T)) * 1.0e-3 / eVtokJ : tof;
+        if (a.tof && !keep)
+            a.tof[c] = a.want_activity ? (log((hP * tof) / (kB * T)) * (Rgas * T)) * 1.0e-3 / eVtokJ : tof;
         if (a.status) a.status[c] = st;
         if (a.nsteps) a.nsteps[c] = a.retry_pass ? a.nsteps[c] + ns : ns;
     }

@@ -700,8 +700,11 @@ __global__ void __launch_bounds__(1024) k_wave_order(int64_t n, int64_t W, const
 }
 
 // One solver launch over the batch (lane or lane-group path).
+// lanes > 0 (lane path with an index list of known length): launch only that
+// many lanes instead of n * G
 static int run_solver(const pck_network* net, const pck_conditions* cond, const SolveArgs& a_in, bool grp,
-                      GrpArgs& ga, bool traj, const double* kf, const double* kr, hipStream_t s) {
+                      GrpArgs& ga, bool traj, const double* kf, const double* kr, hipStream_t s,
+                      int64_t lanes_override = 0) {
     SolveArgs a = a_in;
     const int64_t n = cond->n;
     int rc;
@@ -759,7 +762,7 @@ static int run_solver(const pck_network* net, const pck_conditions* cond, const 
     }
     const int B = PCK_SOLVE_BLOCK;
     const int R = net->nv.NRXN;
-    const int64_t lanes = n * a.G;
+    const int64_t lanes = (lanes_override > 0 && !grp) ? lanes_override : n * a.G;
     const size_t shm = lds_bytes(R, net->nv.NDYN, B);
     dim3 g((unsigned)((lanes + B - 1) / B));
     if (traj) {
@@ -878,7 +881,7 @@ static int launch_solve(const pck_network* net, const pck_conditions* cond, cons
         pv.max_steps = a.max_steps < 1000 ? a.max_steps : 1000;
         pv.y = nullptr; pv.tof = nullptr; pv.status = nullptr; pv.nsteps = pns;
         pv.idx = list; pv.nidx = cnt; pv.retry_pass = 0; pv.worder = nullptr;
-        rc = run_solver(net, cond, pv, grp, ga, traj, kf, kr, s);
+        rc = run_solver(net, cond, pv, grp, ga, traj, kf, kr, s, W * PCK_PREVIEW_LANES);
         if (rc) return rc;
         hipLaunchKernelGGL(k_wave_order, dim3(1), dim3(1024), 0, s, n, W, pns, wo);
         HIPCHK(hipGetLastError());

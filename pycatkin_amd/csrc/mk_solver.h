@@ -996,15 +996,18 @@ __global__ void __launch_bounds__(PCK_SOLVE_BLOCK) __attribute__((amdgpu_waves_p
         for (int i = 0; i < NS; ++i) fin = fin && isfinite(y[i]);
         if (!fin && st == PCK_ST_OK) st = PCK_ST_NONFINITE;
         if (!drc) {
-            if (a.y) {
+            // retry pass: a completed transient is the degenerate root's answer;
+            // a failed one keeps the first pass's outputs (PCK_ST_NEWTON_LOOSE)
+            const bool keep = a.retry_pass && st != PCK_ST_OK;
+            if (a.retry_pass) st = keep ? PCK_ST_NEWTON_LOOSE : PCK_ST_NEWTON;
+            if (a.y && !keep) {
 #pragma unroll
                 for (int i = 0; i < NS; ++i) a.y[i * a.ld_y + c] = y[i];
             }
-            if (a.tof) {
+            if (a.tof && !keep) {
                 // old_system.py:526-527
                 a.tof[c] = a.want_activity ? (log((hP * tof) / (kB * T)) * (Rgas * T)) * 1.0e-3 / eVtokJ : tof;
             }
-            if (a.retry_pass && st == PCK_ST_OK) st = PCK_ST_NEWTON;   // the transient of a degenerate root
             if (a.status) a.status[c] = st;
             if (a.nsteps) a.nsteps[c] = a.retry_pass ? a.nsteps[c] + ns : ns;
         }

@@ -292,7 +292,9 @@ def test_synthetic_steady_vs_oracle(P, synthetic):
     r = sim.solve_batch(T=np.full(n, 500.0), desc={'D%d' % k: D[:, k] for k in range(4)}, tof_terms=('R0',),
                         steady=True, max_steps=20000)
     st = r['status']
-    assert np.mean(st == 0) > 0.3 and np.mean((st == 0) | (st == 4)) > 0.99, np.unique(st, return_counts=True)
+    # 5: a degenerate root whose tight retry failed, reported at the input tolerances
+    assert np.mean(st == 0) > 0.3 and np.mean((st == 0) | (st == 4) | (st == 5)) > 0.99, \
+        np.unique(st, return_counts=True)
     dyn = None
     for c in (np.flatnonzero(st == 0)[0], np.flatnonzero(st == 4)[0]):
         m = O.ClassicModel(spec_of(net, D[c]), T=500.0)
@@ -528,7 +530,7 @@ def test_synthetic_former_stragglers_vs_oracle(P, synthetic):
         st = int(r['status'][j])
         dyn = [names.index(nm) for nm in plan.dyn]
         if not bdf_ok:                         # the reference path has no answer here
-            assert st in (0, 4), (idx[j], st)
+            assert st in (0, 4, 5), (idx[j], st)
             continue
         if st == 0 and not regular:
             # the device's Newton converged where the oracle's (from scipy's
