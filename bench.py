@@ -519,7 +519,8 @@ def build_parser():
     ap.add_argument('--n', type=int, default=0, help='conditions of the non-volcano configs (0: config default)')
     ap.add_argument('--max-steps', type=int, default=200000, help='integrator step budget per condition (library default)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--cpu-points', type=int, default=160)
+    ap.add_argument('--cpu-points', type=int, default=4000,
+                    help='CPU baseline sample (stopped after 25 s of wall time)')
     ap.add_argument('--no-newton', action='store_true', help='A/B diagnostic: transient only (not the bench workload)')
     ap.add_argument('--no-retry', action='store_true',
                     help='A/B diagnostic: degenerate roots keep the first transient (not the bench workload)')
@@ -669,7 +670,8 @@ def main(argv=None):
             achieved = fl / (k3_ms * 1e-3) / 1e12
             roof = {'bound': 'mfma' if False else 'valu_fp64', 'achieved': achieved, 'peak': FP64_VECTOR_PEAK_TFLOPS,
                     'unit': 'TFLOP/s', 'frac': achieved / FP64_VECTOR_PEAK_TFLOPS, 'traffic': traffic,
-                    'traffic_unit': 'bytes per launch (rocprofv3 PMC FETCH_SIZE x2 + WRITE_SIZE)',
+                    'traffic_unit': 'bytes per step over the solver launches (rocprofv3 PMC FETCH_SIZE x2 + '
+                                    'WRITE_SIZE, per-launch average x solver launches per step)',
                     'traffic_source': traffic_src, 'algorithmic_bytes': wl.algo_bytes,
                     'kernel': wl.kernel_name, 'kernel_ms': k3_ms, 'rate_constants_ms': k1_ms,
                     'flops_per_launch': fl, 'flops_structural': fl_struct, 'flops_pmc_f64': fl_pmc,

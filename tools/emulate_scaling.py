@@ -27,7 +27,8 @@ def shard_ms(bench, torch, scaling, rank, world, steps):
     args = bench.build_parser().parse_args(['--scaling', scaling])
     wl = bench.volcano_workload(args, rank, world)
     sp = C.c_void_p(torch.cuda.current_stream().cuda_stream)
-    wl.step(sp)
+    for _ in range(3):                 # warm-up: clocks and the pool allocator settle
+        wl.step(sp)
     torch.cuda.synchronize()
     ts = []
     for _ in range(steps):
