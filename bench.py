@@ -129,10 +129,21 @@ def cpu_baseline(config, n_points=160, workers=16, seed=0, budget_s=25.0):
         pool.map(_cpu_warm, range(workers))            # imports outside the timed sample
         t = time.time()
         done = 0
-        for _ in pool.imap_unordered(_cpu_point, pts):
-            done += 1
-            if time.time() - t > budget_s:
+        it = pool.imap_unordered(_cpu_point, pts)
+        # the sample ends at budget_s whether or not results keep arriving: a
+        # worker can sit minutes on one stiff point (lsoda crawling through the
+        # O-poisoned corner), and with every worker on one the loop would wait
+        while True:
+            left = budget_s - (time.time() - t)
+            if left <= 0:
                 break
+            try:
+                it.next(timeout=left)
+            except StopIteration:
+                break
+            except mp.TimeoutError:
+                break
+            done += 1
         dt = time.time() - t
     finally:
         pool.terminate()
