@@ -135,6 +135,38 @@ def test_volcano_fixture_parity(P, inputs):
     assert flips.size <= 0.05 * n, info['flips'][:10]
     assert info['flip_rate_uniform_nodes'] <= 0.02, info['flip_rate_uniform_nodes']
     spec = O.load_spec(os.path.join(inputs, 'COOxVolcano', 'input.json'))
+
+    def imbalance(k, yy):
+        """max |f_i| / gross_i over the non-pivot species of the oracle model at state yy"""
+        sp = copy.deepcopy(spec)
+        O.set_volcano_point(sp, eco[k], eo[k])
+        m = O.ClassicModel(sp)
+        full = m.y0.copy()
+        for q, nm in enumerate(names):
+            full[m.idx[nm]] = yy[q]
+        f, g = np.abs(m.rhs(full))[m.dyn], m.gross_flux(full)[m.dyn]
+        keep = np.ones(len(m.dyn), bool)
+        keep[list(O._rref(m.conservation())[1])] = False
+        return float(np.max(np.where(g[keep] > 0, f[keep] / np.where(g[keep] > 0, g[keep], 1.0), 0.0)))
+
+    # the reference's own steady-state algorithm (find_steady: least_squares
+    # from its lsoda transient, old_system.py:426-433) against the device's
+    # regular roots: equal to 1e-6 on log10 TOF at most nodes; where not, the
+    # device's state balances every species of the reference's equations (the
+    # record says how often least_squares' answer does not: stopped at xtol)
+    both_ok = both & fx['ok'] & np.isfinite(fx['l10_ls'])
+    ls_err = np.abs(fx['l10_ls'] - l10) / np.abs(l10)
+    agree = both_ok & (ls_err <= RTOL)
+    info['least_squares_agrees_on_regular'] = float(agree.sum() / max(both_ok.sum(), 1))
+    worse = []
+    for k in np.nonzero(both_ok & ~agree)[0][:40]:
+        worse.append((imbalance(k, fx['y_ls'][k]), imbalance(k, y[k])))
+    info['disagreeing_least_squares_vs_device_imbalance'] = worse
+    _record('volcano_fixture_parity.json', info)
+    assert info['least_squares_agrees_on_regular'] >= 0.85, info['least_squares_agrees_on_regular']
+    info['disagreeing_least_squares_also_a_root'] = int(sum(ref <= 1e-8 for ref, dev in worse))
+    _record('volcano_fixture_parity.json', info)
+    assert all(dev <= 1e-10 for ref, dev in worse), worse[:5]
     for k in flips:
         if st[k] == 0:
             sp = copy.deepcopy(spec)

@@ -12,6 +12,7 @@
 #   smoke              __graft_entry__.smoke()               -> OUT/smoke.log
 #   bench:ARGS         python bench.py ARGS (',' = ' ')      -> OUT/bench_<n>.json / .err
 #   benchlong:ARGS     the same with a 1000 s limit (synthetic 1e6)
+#   abbench:NAME:ARGS  bench.py ARGS on the A/B build pycatkin_amd/_ab/lib_NAME.so
 #   py:SCRIPT,ARGS     python SCRIPT ARGS                    -> OUT/py_<n>.log
 #   profile:NAME:ARGS  tools/profile.sh OUT/NAME python3 bench.py ARGS
 #   ab:NAME,NAME...    tools/ab_run.sh variants (pycatkin_amd/_ab/lib_NAME.so)
@@ -37,6 +38,11 @@ for step in "$@"; do
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/$OUT/smoke.log 2>&1 ;;
     bench)
       timeout -k 10 400 python -u bench.py ${arg//,/ } > gpurun_out/$OUT/bench_$k.json 2> gpurun_out/$OUT/bench_$k.err ;;
+    abbench)            # abbench:NAME:ARGS -- bench.py ARGS on pycatkin_amd/_ab/lib_NAME.so
+      name=${arg%%:*}
+      bargs=${arg#*:}
+      PCK_LIB=$PWD/pycatkin_amd/_ab/lib_$name.so timeout -k 10 400 python -u bench.py ${bargs//,/ } \
+          > gpurun_out/$OUT/bench_$k.json 2> gpurun_out/$OUT/bench_$k.err ;;
     benchlong)
       timeout -k 10 1000 python -u bench.py ${arg//,/ } > gpurun_out/$OUT/bench_$k.json 2> gpurun_out/$OUT/bench_$k.err ;;
     py)

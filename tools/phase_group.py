@@ -20,6 +20,13 @@ sys.path.insert(0, ROOT)
 
 
 def main():
+    # --lib PATH (the PCK_TRACE build); the compiled-in kernels carry the
+    # phase counters, so the hipRTC path is switched off here
+    if '--lib' in sys.argv:
+        i = sys.argv.index('--lib')
+        os.environ['PCK_LIB'] = os.path.abspath(sys.argv[i + 1])
+        del sys.argv[i:i + 2]
+    os.environ['PCK_JIT'] = '0'
     import torch
     import pycatkin_amd as P
     from pycatkin_amd import _lib as L
