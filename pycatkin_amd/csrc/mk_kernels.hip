@@ -699,6 +699,54 @@ __global__ void __launch_bounds__(1024) k_wave_order(int64_t n, int64_t W, const
     for (int64_t w = tid; w < W; w += 1024) order[atomicAdd(&base[key(w)], 1)] = (int32_t)w;
 }
 
+// The retry list of the wavefronts at positions [0, nw) of a dispatch order
+// (k_select_status restricted to them): one wave of threads per wavefront.
+__global__ void __launch_bounds__(256) k_select_ordered(int64_t n, const int32_t* wo, int64_t nw,
+                                                        const int32_t* status, int32_t want, int64_t* idx,
+                                                        int32_t* cnt) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t p = t >> 6;
+    const int lane = threadIdx.x & 63;
+    const int64_t c = (p < nw) ? (int64_t)wo[p] * PCK_SOLVE_BLOCK + lane : n;
+    const bool f = (c < n) && status[c] == want;
+    const unsigned long long m = __ballot(f);
+    if (m == 0ull) return;                             // wave-uniform
+    int base = 0;
+    if (lane == 0) base = atomicAdd(cnt, (int)__popcll(m));
+    base = __shfl(base, 0, 64);
+    if (f) idx[base + __popcll(m & ((1ull << lane) - 1ull))] = c;
+}
+
+// A second stream (and two events) per host thread and device, for the
+// degenerate-root retry of the first wavefronts of an ordered first pass to
+// run beside the rest of it; never destroyed (process lifetime).
+struct SideStream {
+    hipStream_t s = nullptr;
+    hipEvent_t first = nullptr, done = nullptr;
+};
+static int side_stream(SideStream** out) {
+    static thread_local SideStream ss[64];
+    int dev = 0;
+    HIPCHK(hipGetDevice(&dev));
+    if (dev < 0 || dev >= 64) return fail(PCK_E_HIP, "device index%s out of range", "");
+    SideStream& x = ss[dev];
+    if (!x.s) {
+        HIPCHK(hipStreamCreateWithFlags(&x.s, hipStreamNonBlocking));
+        HIPCHK(hipEventCreateWithFlags(&x.first, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&x.done, hipEventDisableTiming));
+    }
+    *out = &x;
+    return PCK_OK;
+}
+
+// Fraction of the ordered wavefronts (the cheapest, dispatched last) whose
+// first pass runs beside the retry of the others (PCK_RETRY_OVERLAP, 0 = off).
+static double retry_overlap() {
+    const char* e = getenv("PCK_RETRY_OVERLAP");
+    const double v = e ? atof(e) : 0.3;
+    return (v > 0.0 && v < 1.0) ? v : 0.0;
+}
+
 // One solver launch over the batch (lane or lane-group path).
 // lanes > 0 (lane path with an index list of known length): launch only that
 // many lanes instead of n * G
@@ -823,7 +871,7 @@ static int launch_solve(const pck_network* net, const pck_conditions* cond, cons
     a.idx = nullptr; a.nidx = nullptr; a.retry_pass = 0; a.worder = nullptr;
     // degenerate roots (status 4) are re-integrated by a second launch over
     // their compacted list (pck_solve only: G == 1, no DRC groups)
-    const bool retry = prm->newton && prm->retry_rtol > 0.0 && !drc_groups && a.G == 1;
+    bool retry = prm->newton && prm->retry_rtol > 0.0 && !drc_groups && a.G == 1;
     const bool traj = (prm->n_out > 0 && a.traj != nullptr);
     if (traj) {
         if (!prm->t_out) return fail(PCK_E_ARG, "n_out > 0 without t_out%s", "");
@@ -891,16 +939,67 @@ static int launch_solve(const pck_network* net, const pck_conditions* cond, cons
     if (retry) {
         // the retry list (int64 per condition), its length, and a status
         // array when the caller passed none
-        const size_t bytes = sizeof(int64_t) * (size_t)n + 64 + (a.status ? 0 : sizeof(int32_t) * (size_t)n);
+        // (W wavefronts' worth of entries: the overlapped split keeps two lists)
+        const size_t nl = (size_t)((n + PCK_SOLVE_BLOCK - 1) / PCK_SOLVE_BLOCK) * PCK_SOLVE_BLOCK;
+        const size_t bytes = sizeof(int64_t) * nl + 64 + (a.status ? 0 : sizeof(int32_t) * (size_t)n);
         rc = salloc(rscr, bytes, s);
         if (rc) return rc;
-        if (!a.status) a.status = (int32_t*)(rscr.as<char>() + sizeof(int64_t) * (size_t)n + 64);
+        if (!a.status) a.status = (int32_t*)(rscr.as<char>() + sizeof(int64_t) * nl + 64);
     }
-    rc = run_solver(net, cond, a, grp, ga, traj, kf, kr, s);
-    if (rc) return rc;
+    const double ovl = (retry && a.worder) ? retry_overlap() : 0.0;
+    if (ovl > 0.0) {
+        // ordered first pass in two launches: the first K wavefronts (the
+        // costliest), then the rest; the retry of the first K runs on a side
+        // stream beside the second launch, the retry of the rest after it
+        const int64_t W = (n + PCK_SOLVE_BLOCK - 1) / PCK_SOLVE_BLOCK;
+        int64_t K = W - (int64_t)(ovl * (double)W);
+        K = K < 1 ? 1 : (K > W - 1 ? W - 1 : K);
+        SideStream* ss = nullptr;
+        rc = side_stream(&ss);
+        if (rc) return rc;
+        int64_t* list1 = rscr.as<int64_t>();
+        int64_t* list2 = list1 + K * PCK_SOLVE_BLOCK;
+        int32_t* cnt = (int32_t*)(list1 + W * PCK_SOLVE_BLOCK);
+        HIPCHK(hipMemsetAsync(cnt, 0, 2 * sizeof(int32_t), s));
+        SolveArgs r = a;
+        r.rtol = prm->retry_rtol;
+        r.atol = prm->retry_atol;
+        r.newton = 0;
+        r.retry_pass = 1;
+        r.worder = nullptr;
+        const int32_t* wo = a.worder;
+        rc = run_solver(net, cond, a, grp, ga, traj, kf, kr, s, K * PCK_SOLVE_BLOCK);
+        if (rc) return rc;
+        HIPCHK(hipEventRecord(ss->first, s));
+        HIPCHK(hipStreamWaitEvent(ss->s, ss->first, 0));
+        hipLaunchKernelGGL(k_select_ordered, dim3((unsigned)((K * 64 + 255) / 256)), dim3(256), 0, ss->s, n, wo, K,
+                           a.status, (int32_t)PCK_ST_NEWTON, list1, cnt);
+        HIPCHK(hipGetLastError());
+        r.idx = list1;
+        r.nidx = cnt;
+        rc = run_solver(net, cond, r, grp, ga, traj, kf, kr, ss->s, K * PCK_SOLVE_BLOCK);
+        if (rc) return rc;
+        HIPCHK(hipEventRecord(ss->done, ss->s));
+        SolveArgs a2 = a;
+        a2.worder = wo + K;
+        rc = run_solver(net, cond, a2, grp, ga, traj, kf, kr, s, (W - K) * PCK_SOLVE_BLOCK);
+        if (rc) return rc;
+        hipLaunchKernelGGL(k_select_ordered, dim3((unsigned)(((W - K) * 64 + 255) / 256)), dim3(256), 0, s, n,
+                           wo + K, W - K, a.status, (int32_t)PCK_ST_NEWTON, list2, cnt + 1);
+        HIPCHK(hipGetLastError());
+        r.idx = list2;
+        r.nidx = cnt + 1;
+        rc = run_solver(net, cond, r, grp, ga, traj, kf, kr, s, (W - K) * PCK_SOLVE_BLOCK);
+        if (rc) return rc;
+        HIPCHK(hipStreamWaitEvent(s, ss->done, 0));        // the caller's stream sees both retries
+        retry = false;                                     // done
+    } else {
+        rc = run_solver(net, cond, a, grp, ga, traj, kf, kr, s);
+        if (rc) return rc;
+    }
     if (retry) {
         int64_t* idx = rscr.as<int64_t>();
-        int32_t* cnt = (int32_t*)(idx + n);
+        int32_t* cnt = (int32_t*)(idx + ((n + PCK_SOLVE_BLOCK - 1) / PCK_SOLVE_BLOCK) * PCK_SOLVE_BLOCK);
         HIPCHK(hipMemsetAsync(cnt, 0, sizeof(int32_t), s));
         hipLaunchKernelGGL(k_select_status, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, a.status,
                            (int32_t)PCK_ST_NEWTON, idx, cnt);
