@@ -741,9 +741,13 @@ static int side_stream(SideStream** out) {
 
 // Fraction of the ordered wavefronts (the cheapest, dispatched last) whose
 // first pass runs beside the retry of the others (PCK_RETRY_OVERLAP, 0 = off).
+// Off by default: on the 1024^2 volcano the split costs more than it hides
+// (r3s A/B: 7.50 ms off; 8.14 / 8.07 / 8.36 / 8.99 ms at 0.2 / 0.3 / 0.45 / 0.6)
+// because the second half-launch starts with a cold tail of 1-step waves and
+// the retry waves then compete with it for the same CUs.
 static double retry_overlap() {
     const char* e = getenv("PCK_RETRY_OVERLAP");
-    const double v = e ? atof(e) : 0.3;
+    const double v = e ? atof(e) : 0.0;
     return (v > 0.0 && v < 1.0) ? v : 0.0;
 }
 
