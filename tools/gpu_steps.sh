@@ -14,6 +14,7 @@
 #   benchlong:ARGS     the same with a 1000 s limit (synthetic 1e6)
 #   abbench:NAME:ARGS  bench.py ARGS on the A/B build pycatkin_amd/_ab/lib_NAME.so
 #   envbench:V=X:ARGS  bench.py ARGS with the environment variable V=X
+#   abenv:NAME:V=X:ARGS  abbench with the environment variable V=X
 #   py:SCRIPT,ARGS     python SCRIPT ARGS                    -> OUT/py_<n>.log
 #   profile:NAME:ARGS  tools/profile.sh OUT/NAME python3 bench.py ARGS
 #   ab:NAME,NAME...    tools/ab_run.sh variants (pycatkin_amd/_ab/lib_NAME.so)
@@ -48,6 +49,13 @@ for step in "$@"; do
       kv=${arg%%:*}
       bargs=${arg#*:}
       env "$kv" timeout -k 10 400 python -u bench.py ${bargs//,/ } \
+          > gpurun_out/$OUT/bench_$k.json 2> gpurun_out/$OUT/bench_$k.err ;;
+    abenv)              # abenv:NAME:VAR=VALUE:ARGS -- abbench with one environment variable set
+      name=${arg%%:*}
+      rest=${arg#*:}
+      kv=${rest%%:*}
+      bargs=${rest#*:}
+      env "$kv" PCK_LIB=$PWD/pycatkin_amd/_ab/lib_$name.so timeout -k 10 400 python -u bench.py ${bargs//,/ } \
           > gpurun_out/$OUT/bench_$k.json 2> gpurun_out/$OUT/bench_$k.err ;;
     benchlong)
       timeout -k 10 1000 python -u bench.py ${arg//,/ } > gpurun_out/$OUT/bench_$k.json 2> gpurun_out/$OUT/bench_$k.err ;;
