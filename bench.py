@@ -391,10 +391,13 @@ def cstr_workload(args, rank, world):
     sim = P.read_from_input_file(os.path.join(INPUTS, 'COOxReactor', 'input_Pd111.json'))
     plan = sim.plan(('CO_ox',))
     net = sim.device(('CO_ox',))
+    if args.group:
+        net.set_plan_mode(2)
     n_tot = args.n or 10000
     T = _shard(np.linspace(423.0, 623.0, n_tot if args.scaling == 'strong' else n_tot * world), rank, world)
     _solve_workload(wl, sim, net, plan, T.size, T, None, None, ('CO_ox',), True, False, args=args)
-    wl.kernel_name = 'k_solve<PlanCT<CstrPd111>>' if net.compiled_plan else 'k_solve<PlanRT<6>>'
+    wl.kernel_name = ('k_solve_grp<6, 16>' if args.group else
+                      'k_solve<PlanCT<CstrPd111>>' if net.compiled_plan else 'k_solve<PlanRT<6>>')
     wl.tag = 'cstr %d' % n_tot
     wl.config = {'workload': 'COOxReactor Pd111 CSTR temperature sweep: %d temperatures 423-623 K, t_end 3600 s '
                              '(input rtol 1e-8 / atol 1e-10) + Newton steady state' % n_tot,
@@ -544,6 +547,8 @@ def build_parser():
                     help="condition order in HBM: 'tile' = one grid patch per wave (default), 'row' = row-major")
     ap.add_argument('--runtime-plan', action='store_true',
                     help='A/B: force the runtime-plan solver instead of the compiled-in network')
+    ap.add_argument('--group', action='store_true',
+                    help='A/B (cstr): one 16-lane group per condition (the lane-group solver) instead of one lane')
     ap.add_argument('--device', choices=('gpu', 'cpu-standin'), default='gpu', help=argparse.SUPPRESS)
     return ap
 
