@@ -673,45 +673,33 @@ __global__ void __launch_bounds__(256) k_preview_list(int64_t n, int64_t W, int6
     if (i == 0) *cnt = (int32_t)(W * PCK_PREVIEW_LANES);
 }
 
-// descending counting sort of the wavefronts by their preview key, over the
-// whole grid: histogram (global atomics), one block's scan of the 1024 bins,
-// scatter.  (One 1024-thread block doing all three took 70 us of the 7.5 ms
-// volcano step.)  The order inside a bin follows the atomics; no lane's
-// result depends on it.
-__device__ __forceinline__ int wave_key(int64_t n, int64_t w, const int32_t* ns) {
-    int k = 0;
-    for (int l = 0; l < PCK_PREVIEW_LANES; ++l) {
-        int64_t c = w * PCK_SOLVE_BLOCK + preview_lane(l);
-        c = (c < n) ? c : n - 1;
-        k = max(k, ns[c]);
-    }
-    return min(max(k, 0), 1023);
-}
-
-__global__ void __launch_bounds__(256) k_wave_hist(int64_t n, int64_t W, const int32_t* ns, int32_t* hist) {
-    const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (w < W) atomicAdd(&hist[wave_key(n, w, ns)], 1);
-}
-
-__global__ void __launch_bounds__(1024) k_wave_scan(int32_t* hist) {
-    // exclusive scan from the top bin down (descending keys first), in place
-    __shared__ int v[1024];
-    const int t = threadIdx.x;
-    v[t] = hist[1023 - t];
+// descending counting sort of the wavefronts by their preview key (one block).
+// (A grid-wide histogram / scan / scatter took 0.17 ms against this block's
+// 0.07 ms -- its global atomics contend on a few hundred bins -- and its
+// order inside a bin cost the first pass 0.15 ms more: profiles/r3/wave_sort_ab.)
+__global__ void __launch_bounds__(1024) k_wave_order(int64_t n, int64_t W, const int32_t* ns, int32_t* order) {
+    __shared__ int hist[1024];
+    __shared__ int base[1024];
+    const int tid = threadIdx.x;
+    hist[tid] = 0;
     __syncthreads();
-    for (int d = 1; d < 1024; d <<= 1) {
-        const int x = (t >= d) ? v[t - d] : 0;
-        __syncthreads();
-        v[t] += x;
-        __syncthreads();
+    auto key = [&](int64_t w) {
+        int k = 0;
+        for (int l = 0; l < PCK_PREVIEW_LANES; ++l) {
+            int64_t c = w * PCK_SOLVE_BLOCK + preview_lane(l);
+            c = (c < n) ? c : n - 1;
+            k = max(k, ns[c]);
+        }
+        return min(max(k, 0), 1023);
+    };
+    for (int64_t w = tid; w < W; w += 1024) atomicAdd(&hist[key(w)], 1);
+    __syncthreads();
+    if (tid == 0) {
+        int sum = 0;
+        for (int k = 1023; k >= 0; --k) { base[k] = sum; sum += hist[k]; }
     }
-    hist[1023 - t] = (t > 0) ? v[t - 1] : 0;
-}
-
-__global__ void __launch_bounds__(256) k_wave_scatter(int64_t n, int64_t W, const int32_t* ns, int32_t* base,
-                                                      int32_t* order) {
-    const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (w < W) order[atomicAdd(&base[wave_key(n, w, ns)], 1)] = (int32_t)w;
+    __syncthreads();
+    for (int64_t w = tid; w < W; w += 1024) order[atomicAdd(&base[key(w)], 1)] = (int32_t)w;
 }
 
 // The retry list of the wavefronts at positions [0, nw) of a dispatch order
@@ -932,7 +920,7 @@ static int launch_solve(const pck_network* net, const pck_conditions* cond, cons
     if (order) {
         const int64_t W = (n + PCK_SOLVE_BLOCK - 1) / PCK_SOLVE_BLOCK;
         const size_t b_list = sizeof(int64_t) * (size_t)W * PCK_PREVIEW_LANES, b_ns = sizeof(int32_t) * (size_t)n;
-        rc = salloc(oscr, b_list + 64 + b_ns + sizeof(int32_t) * (size_t)W + sizeof(int32_t) * 1024, s);
+        rc = salloc(oscr, b_list + 64 + b_ns + sizeof(int32_t) * (size_t)W, s);
         if (rc) return rc;
         int64_t* list = oscr.as<int64_t>();
         int32_t* cnt = (int32_t*)((char*)list + b_list);
@@ -950,12 +938,7 @@ static int launch_solve(const pck_network* net, const pck_conditions* cond, cons
         pv.idx = list; pv.nidx = cnt; pv.retry_pass = 0; pv.worder = nullptr;
         rc = run_solver(net, cond, pv, grp, ga, traj, kf, kr, s, W * PCK_PREVIEW_LANES);
         if (rc) return rc;
-        int32_t* hist = wo + W;
-        const unsigned gw = (unsigned)((W + 255) / 256);
-        HIPCHK(hipMemsetAsync(hist, 0, sizeof(int32_t) * 1024, s));
-        hipLaunchKernelGGL(k_wave_hist, dim3(gw), dim3(256), 0, s, n, W, pns, hist);
-        hipLaunchKernelGGL(k_wave_scan, dim3(1), dim3(1024), 0, s, hist);
-        hipLaunchKernelGGL(k_wave_scatter, dim3(gw), dim3(256), 0, s, n, W, pns, hist, wo);
+        hipLaunchKernelGGL(k_wave_order, dim3(1), dim3(1024), 0, s, n, W, pns, wo);
         HIPCHK(hipGetLastError());
         a.worder = wo;
     }
