@@ -67,10 +67,12 @@ def gpu_lu_solve(W, rhs_list):
 
 
 def rodas4(f, J, y, t0, t_end, rtol, atol, cons=None, max_steps=200000, cons_rows=None, trace=None, gpu_lu=False,
-           t_out=None, samples=None):
+           t_out=None, samples=None, ctrl='std'):
     """Returns (y, status, nsteps).  cons: conservation matrix (rows >= 0 get
     the multiplicative projection).  cons_rows: optional (C, piv) -- replace the
-    pivot rows of W by the conservation rows (the index-reduced stage system)."""
+    pivot rows of W by the conservation rows (the index-reduced stage system).
+    ctrl: 'std' (the device's controller) or 'pred' (Gustafsson's predictive
+    controller, Hairer & Wanner's RODAS: A/B only)."""
     NS = y.size
     F0 = f(y)
     span = t_end - t0
@@ -87,6 +89,7 @@ def rodas4(f, J, y, t0, t_end, rtol, atol, cons=None, max_steps=200000, cons_row
     t = t0
     n = 0
     ko = 0
+    hacc, erracc, rejected = None, None, False
     if t_out is not None:
         while ko < len(t_out) and t_out[ko] <= t0:
             samples.append(y.copy())
@@ -177,8 +180,19 @@ def rodas4(f, J, y, t0, t_end, rtol, atol, cons=None, max_steps=200000, cons_row
                 if np.any(neg):
                     y = np.where(neg, 0.0, y)
                     F0 = f(y)
-            h *= min(6.0, max(0.2, fac))
+            m = min(6.0, max(0.2, fac))
+            if ctrl == 'pred':
+                err = max(np.sqrt(q), 1e-300)
+                if hacc is not None:
+                    mg = 0.9 * (h / hacc) * (erracc / err ** 2) ** 0.25
+                    m = min(m, min(6.0, max(0.2, mg)))
+                hacc, erracc = h, max(1e-2, err)
+                if rejected:
+                    m = min(m, 1.0)
+                rejected = False
+            h *= m
         else:
+            rejected = True
             h *= max(0.2, fac) if fin else 0.25
         if not (h > 2.220446049250313e-15 * max(abs(t), 1e-300)) and t < t_end:
             return y, 2, n
