@@ -61,13 +61,30 @@ __device__ double pck_phase[8];
 //          entry {a = r | np << 9 | dptr << 12 | q5 << 26,
 //                 b = q0 | q1 << 6 | q2 << 12 | q3 << 18 | q4 << 24, s (lo, hi)}
 //          with q0..q5 the participants of reaction r (as in rx[r])
+//   sch[LS][G], xbe[2 NS], xrows[NXR]: the balanced walk of the CSR (LS > 0;
+//          built by pck_network_create).  A species row longer than
+//          ceil(NE / G) entries is cut into pieces; the pieces are packed onto
+//          the G lanes of a group longest-first, so every lane walks at most
+//          LS entries instead of the longest row (CH4: 35, synthetic: 56).
+//          Word t of lane l: entry e (bits 0-13) | slot (14-23) | last entry
+//          of its piece (30) | valid (31).  Slot i < NS is row i's first
+//          piece, slot NS + x its extra piece x; row i's extras are
+//          [xbe[2i], xbe[2i+1]), and xrows lists the rows that have any.
+//          Sums run piece by piece in entry order, then over the pieces in
+//          order: deterministic, the same in every build of one network.
 struct GrpView {
     const uint4* rx;
     const int32_t* row;
     const uint4* ent;
     int ND;                  // total participants = size of the derivative buffer
     int NE;                  // entries of the species CSR (= row[NS])
+    const uint32_t* sch;     // balanced walk (LS = 0: off, the per-row loops)
+    const int32_t* xbe;
+    const int32_t* xrows;
+    int LS, NX, NXR;
 };
+#define PCK_SCH_VALID 0x80000000u
+#define PCK_SCH_LAST 0x40000000u
 
 // The solver kernel (TAB = true) copies the tables into LDS once per block
 // (shared by the block's groups): every rate / Jacobian evaluation walks
@@ -75,8 +92,10 @@ struct GrpView {
 // instead of an L1/L2 one.  The host picks TAB only where the extra LDS does
 // not lower the kernel's occupancy (csrc/mk_kernels.hip: grp_tables_pay).
 // Layout (16-byte units): rx[max(R,1)] | ent[max(NE,1)] | row[NS+1] (int32)
-__host__ __device__ inline size_t grp_tab_doubles(int R, int NE, int NS) {
-    const size_t b = 16 * (size_t)(R > 0 ? R : 1) + 16 * (size_t)(NE > 0 ? NE : 1) + 4 * (size_t)(NS + 1);
+// | sch[NSCH] (uint32, the balanced walk's words, NSCH = LS * G)
+__host__ __device__ inline size_t grp_tab_doubles(int R, int NE, int NS, int NSCH = 0) {
+    const size_t b = 16 * (size_t)(R > 0 ? R : 1) + 16 * (size_t)(NE > 0 ? NE : 1) + 4 * (size_t)(NS + 1) +
+                     4 * (size_t)NSCH;
     return (b + 15) / 16 * 2;
 }
 
@@ -293,9 +312,10 @@ __device__ __forceinline__ void rec_drates(const uint4& rec, double kf, double k
 }
 
 __host__ __device__ constexpr int grp_even(int n) { return (n + 1) & ~1; }
-__host__ __device__ inline size_t grp_lds_doubles(int R, int NSP, int NS, int ND, int QB) {
+__host__ __device__ inline size_t grp_lds_doubles(int R, int NSP, int NS, int ND, int QB, int LS = 0, int NX = 0) {
     const int r1 = R > 0 ? R : 1;
-    return (size_t)2 * grp_even(r1) + grp_even(NSP) + grp_even(ND > r1 ? ND : r1) + grp_even(NS * QB) + grp_even(NSP);
+    return (size_t)2 * grp_even(r1) + grp_even(NSP) + grp_even(ND > r1 ? ND : r1) + grp_even(NS * QB) + grp_even(NSP) +
+           (LS ? grp_even(NX * NS) + grp_even(NS + NX) : 0);
 }
 
 // Per-group context: LDS blocks and this lane's species row.
@@ -309,6 +329,9 @@ struct Grp {
     double* d;                // net rates [R] / derivatives [ND]
     double* J;                // Jacobian column block: J[i*QB + j]
     double* pb;               // pivot-row broadcast
+    double* Jx;               // balanced walk: Jacobian rows of the extra pieces [NX][NS]
+    double* part;             // balanced walk: rate sums of the pieces [NS + NX]
+    int xb, xe;               // balanced walk: this row's extra pieces
     int rb, re;               // this row's CSR range
     double cfi, rs, fl, in;   // this row's concentration factor, row scale, flow, inflow
 };
@@ -352,6 +375,34 @@ __device__ __forceinline__ double grp_rhs(const GrpView& g, const Grp<NSP>& x, d
     for (int r = x.gl; r < x.R; r += G) x.d[r] = rec_rate(g.rx[r], x.kf[r], x.kr[r], x.c);
     wsync();
     double f = 0.0;
+    if (g.LS) {
+        // balanced walk: every lane sums its pieces, the row's lane adds them up
+        // the next word and its entry are fetched one iteration ahead (an
+        // invalid word's entry index is 0: a harmless load)
+        double acc = 0.0;
+        uint32_t w = g.sch[x.gl];
+        uint4 q = g.ent[w & 0x3fffu];
+        for (int t = 0; t < g.LS; ++t) {
+            const uint32_t wn = (t + 1 < g.LS) ? g.sch[(t + 1) * G + x.gl] : 0u;
+            const uint4 qn = g.ent[wn & 0x3fffu];
+            if (w & PCK_SCH_VALID) {
+                acc = fma(ent_s(q), x.d[ent_r(q)], acc);
+                if (w & PCK_SCH_LAST) {
+                    x.part[(w >> 14) & 0x3ffu] = acc;
+                    acc = 0.0;
+                }
+            }
+            w = wn;
+            q = qn;
+        }
+        wsync();
+        if (x.row) {
+            f = (x.re > x.rb) ? x.part[x.gl] : 0.0;
+            for (int p = x.xb; p < x.xe; ++p) f += x.part[x.NS + p];
+            f = f * x.rs + x.fl * (x.in - y);
+        }
+        return f;
+    }
     if (x.row) {
         // two partial sums keep several entry loads in flight
         double f2 = 0.0;
@@ -414,6 +465,53 @@ __device__ __forceinline__ void grp_jac(const NetView& nv, const GrpView& g, con
     wsync();
     const double sc = sgn * x.rs;
     const double dg = shift - sgn * x.fl;
+    if (P == 1 && g.LS) {
+        // balanced walk: each lane adds its pieces' terms into their rows (a
+        // row's first piece into J, extras into Jx: every target row has one
+        // writer), then the extras are folded into J per (row, column)
+        uint32_t w = g.sch[x.gl];
+        uint4 q = g.ent[w & 0x3fffu];
+        for (int t = 0; t < g.LS; ++t) {
+            const uint32_t wn = (t + 1 < g.LS) ? g.sch[(t + 1) * G + x.gl] : 0u;
+            const uint4 qn = g.ent[wn & 0x3fffu];
+            if (w & PCK_SCH_VALID) {
+                const int slot = (int)((w >> 14) & 0x3ffu);
+                double* dst = (slot < x.NS) ? x.J + slot * QB : x.Jx + (slot - x.NS) * x.NS;
+                const double s = ent_s(q);
+                const int np = ent_np(q), dp = ent_dptr(q);
+#pragma unroll
+                for (int k = 0; k < PCK_GRP_NPMAX; ++k) {
+                    if (k < np) {
+                        const int sp = ent_species(q, k);
+                        dst[sp] += s * x.d[dp + k];
+                    }
+                }
+            }
+            w = wn;
+            q = qn;
+        }
+        wsync();
+        for (int it = x.gl; it < g.NXR * x.NS; it += G) {
+            const int i = g.xrows[it / x.NS], j = it % x.NS;
+            double v = x.J[i * QB + j];
+            for (int p = g.xbe[2 * i]; p < g.xbe[2 * i + 1]; ++p) {
+                v += x.Jx[p * x.NS + j];
+                x.Jx[p * x.NS + j] = 0.0;
+            }
+            x.J[i * QB + j] = v;
+        }
+        wsync();
+#pragma unroll
+        for (int q = 0; q < NSP; ++q) {
+            double v = 0.0;
+            if (x.row && q < x.NS) {
+                v = x.J[x.gl * QB + q];
+                x.J[x.gl * QB + q] = 0.0;
+            }
+            W[q] = x.row ? sc * v + (q == x.gl ? dg : 0.0) : 0.0;
+        }
+        return;
+    }
 #pragma unroll
     for (int pass = 0; pass < P; ++pass) {
         const int q0 = pass * QB;
@@ -973,6 +1071,13 @@ __device__ __forceinline__ void grp_setup(const NetView& nv, const GrpView& gv, 
     x.d = x.c + grp_even(NSP);
     x.J = x.d + grp_even(gv.ND > r1 ? gv.ND : r1);
     x.pb = x.J + grp_even(x.NS * QB);
+    x.Jx = x.pb + grp_even(NSP);
+    x.part = x.Jx + grp_even(gv.NX * x.NS);
+    x.xb = x.xe = 0;
+    if (gv.LS) {
+        for (int i = x.gl; i < gv.NX * x.NS; i += G) x.Jx[i] = 0.0;
+        if (x.gl < x.NS) { x.xb = gv.xbe[2 * x.gl]; x.xe = gv.xbe[2 * x.gl + 1]; }
+    }
     T = cv.T[c * cv.sT];
     for (int j = x.gl; j < R; j += G) {
         double a = kf[j * ld_k + c], b = kr[j * ld_k + c];
@@ -1050,10 +1155,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 64
         for (int i = threadIdx.x; i < nv.NRXN; i += 64) trx[i] = gv.rx[i];
         for (int i = threadIdx.x; i < gv.NE; i += 64) tent[i] = gv.ent[i];
         for (int i = threadIdx.x; i <= nv.NDYN; i += 64) trow[i] = gv.row[i];
+        uint32_t* tsch = (uint32_t*)(trow + nv.NDYN + 1);
+        for (int i = threadIdx.x; i < gv.LS * G; i += 64) tsch[i] = gv.sch[i];
         wsync();
         gl.rx = trx;
         gl.ent = tent;
         gl.row = trow;
+        if (gv.LS) gl.sch = tsch;
     }
     if (slot >= cv.n) return;                       // group-uniform exit; no block barriers below
     const int64_t c = slot;
@@ -1063,8 +1171,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 64
     Grp<NSP> x;
     double T;
     grp_setup<NSP, G>(nv, gl, cv, c, kf, kr, ld_k, pj, pfac,
-                      lds + (TAB ? grp_tab_doubles(nv.NRXN, gv.NE, nv.NDYN) : 0) +
-                          (size_t)grp * grp_lds_doubles(nv.NRXN, NSP, nv.NDYN, gv.ND, ga.QB), ga.QB, x, T);
+                      lds + (TAB ? grp_tab_doubles(nv.NRXN, gv.NE, nv.NDYN, gv.LS * G) : 0) +
+                          (size_t)grp * grp_lds_doubles(nv.NRXN, NSP, nv.NDYN, gv.ND, ga.QB, gv.LS, gv.NX), ga.QB, x, T);
     double y = 0.0;
     int ns = 0;
     TrajOut to{a.t_out, a.n_out, a.traj, a.ld_traj, c};
@@ -1132,7 +1240,7 @@ __global__ void __launch_bounds__(64) k_rates_grp(NetView nv, GrpView gv, CondVi
     Grp<NSP> x;
     double T;
     grp_setup<NSP, G>(nv, gv, cv, c, kf, kr, ld_k, -1, 1.0,
-                      lds + (size_t)grp * grp_lds_doubles(nv.NRXN, NSP, nv.NDYN, gv.ND, QB), QB, x, T);
+                      lds + (size_t)grp * grp_lds_doubles(nv.NRXN, NSP, nv.NDYN, gv.ND, QB, gv.LS, gv.NX), QB, x, T);
     const double y = x.row ? yin[x.gl * ld_y + c] : 0.0;
     if (!jac) {
         const double f = grp_rhs<NSP, G>(gv, x, y);

@@ -14,6 +14,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <algorithm>
 #include <atomic>
 #include <mutex>
 #include <new>
@@ -308,14 +309,83 @@ extern "C" int pck_network_create(const int32_t* ip, int64_t n_ip, const double*
         }
         row[NS] = (int32_t)(ent.size() / 4);
         for (int i = 0; i < NS; ++i) net->grp_degmax = std::max(net->grp_degmax, row[i + 1] - row[i]);
+        // balanced walk of the CSR (mk_group.h: GrpView::sch): rows longer than
+        // K = ceil(NE / G) entries are cut into near-equal pieces, the pieces
+        // packed onto the G lanes longest-first (least-loaded lane, lowest id on
+        // ties); taken when it shortens the longest walk (PCK_GRP_BALANCE=0: off)
+        std::vector<uint32_t> sch;
+        std::vector<int32_t> xbe(2 * (size_t)NS, 0), xrows;
+        int LS = 0, NX = 0;
+        {
+            const int NE = row[NS];
+            const int G = NS <= 16 ? 16 : NS <= 32 ? 32 : 64;      // csrc: grp_g
+            const char* eb = getenv("PCK_GRP_BALANCE");
+            if (!(eb && eb[0] == '0') && NE > 0 && NE <= 0x3fff && NS > 0) {
+                const int K = std::max(1, (NE + G - 1) / G);
+                struct Piece { int b, e, slot; };
+                std::vector<Piece> pcs;
+                for (int i = 0; i < NS; ++i) {
+                    const int deg = row[i + 1] - row[i];
+                    if (deg == 0) continue;
+                    const int m = (deg + K - 1) / K;
+                    xbe[2 * i] = NX;
+                    for (int p = 0; p < m; ++p)
+                        pcs.push_back({row[i] + deg * p / m, row[i] + deg * (p + 1) / m, p == 0 ? i : NS + NX++});
+                    xbe[2 * i + 1] = NX;
+                    if (m > 1) xrows.push_back(i);
+                }
+                std::vector<int> ord(pcs.size());
+                for (size_t k = 0; k < ord.size(); ++k) ord[k] = (int)k;
+                std::stable_sort(ord.begin(), ord.end(), [&](int a, int b2) {
+                    return pcs[a].e - pcs[a].b > pcs[b2].e - pcs[b2].b;
+                });
+                std::vector<int> load(G, 0);
+                std::vector<std::vector<int>> lane(G);
+                for (int k : ord) {
+                    int l = 0;
+                    for (int j = 1; j < G; ++j)
+                        if (load[j] < load[l]) l = j;
+                    lane[l].push_back(k);
+                    load[l] += pcs[k].e - pcs[k].b;
+                }
+                for (int l = 0; l < G; ++l) LS = std::max(LS, load[l]);
+                if (LS >= net->grp_degmax || NS + NX > 1023) {
+                    LS = 0;                                 // no gain (or too many slots): the per-row loops
+                } else {
+                    sch.assign((size_t)LS * G, 0u);
+                    for (int l = 0; l < G; ++l) {
+                        int t = 0;
+                        for (int k : lane[l])
+                            for (int e2 = pcs[k].b; e2 < pcs[k].e; ++e2, ++t)
+                                sch[(size_t)t * G + l] = (uint32_t)e2 | ((uint32_t)pcs[k].slot << 14) | PCK_SCH_VALID |
+                                                         (e2 == pcs[k].e - 1 ? PCK_SCH_LAST : 0u);
+                    }
+                }
+            }
+            if (!LS) { NX = 0; xrows.clear(); }
+        }
+        if (sch.empty()) sch.assign(1, 0u);
+        if (xrows.empty()) xrows.assign(1, 0);
+        if (xbe.empty()) xbe.assign(2, 0);
         if (ent.empty()) ent.assign(4, 0u);
         const size_t brx = sizeof(uint32_t) * rx.size(), bent = sizeof(uint32_t) * ent.size();
-        const size_t brow = sizeof(int32_t) * row.size();
+        const size_t brow = sizeof(int32_t) * row.size(), bsch = sizeof(uint32_t) * sch.size();
+        const size_t bxbe = sizeof(int32_t) * xbe.size(), bxr = sizeof(int32_t) * xrows.size();
         char* buf = nullptr;
-        e = hipMalloc((void**)&buf, brx + bent + brow);
+        e = hipMalloc((void**)&buf, brx + bent + brow + bsch + bxbe + bxr);
         if (e == hipSuccess) e = hipMemcpy(buf, rx.data(), brx, hipMemcpyHostToDevice);
         if (e == hipSuccess) e = hipMemcpy(buf + brx, ent.data(), bent, hipMemcpyHostToDevice);
         if (e == hipSuccess) e = hipMemcpy(buf + brx + bent, row.data(), brow, hipMemcpyHostToDevice);
+        size_t o = brx + bent + brow;
+        if (e == hipSuccess) e = hipMemcpy(buf + o, sch.data(), bsch, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpy(buf + o + bsch, xbe.data(), bxbe, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpy(buf + o + bsch + bxbe, xrows.data(), bxr, hipMemcpyHostToDevice);
+        net->gv.sch = (const uint32_t*)(buf + o);
+        net->gv.xbe = (const int32_t*)(buf + o + bsch);
+        net->gv.xrows = (const int32_t*)(buf + o + bsch + bxbe);
+        net->gv.LS = LS;
+        net->gv.NX = NX;
+        net->gv.NXR = LS ? (int)xrows.size() : 0;
         net->d_grp = buf;
         if (e != hipSuccess) {
             (void)hipFree(net->d_ip); (void)hipFree(net->d_dp); (void)hipFree(buf);
@@ -525,8 +595,8 @@ static int grp_shape(const pck_network* net, int nsp, int P, size_t* shm, int* Q
     const int NS = net->nv.NDYN;
     const int per = 64 / grp_g(NS);
     *QB = (nsp + P - 1) / P;
-    *shm = sizeof(double) * per * grp_lds_doubles(net->nv.NRXN, nsp, NS, net->gv.ND, *QB);
-    if (tables) *shm += sizeof(double) * grp_tab_doubles(net->nv.NRXN, net->gv.NE, NS);   // k_solve_grp
+    *shm = sizeof(double) * per * grp_lds_doubles(net->nv.NRXN, nsp, NS, net->gv.ND, *QB, net->gv.LS, net->gv.NX);
+    if (tables) *shm += sizeof(double) * grp_tab_doubles(net->nv.NRXN, net->gv.NE, NS, net->gv.LS * grp_g(NS));
     if (*shm > 64 * 1024)
         return fail(PCK_E_SIZE, "lane-group solver: network needs %s%lld bytes of LDS per wavefront", "", (long long)*shm);
     return PCK_OK;

@@ -551,3 +551,43 @@ def test_synthetic_former_stragglers_vs_oracle(P, synthetic):
         else:   # degenerate root: two integrators' transients at t_end, bounded by their error
             assert close(r['y'][:, j], yT[dyn], rtol=1e-3, floor=1e-9), (idx[j], np.abs(r['y'][:, j] - yT[dyn]).max())
     assert checked >= 2, checked
+
+
+def test_balanced_walk_matches_row_loops(P, inputs, synthetic, monkeypatch):
+    """The balanced walk of the species CSR (mk_group.h GrpView::sch: long
+    rows cut into pieces packed over the group's lanes) against the per-row
+    loops it replaces (PCK_GRP_BALANCE=0 at network creation): the same sums
+    in another order, so rates and Jacobians agree to rounding, and a CH4
+    steady solve lands on the same root.  Both networks use it (CH4 walks
+    17 entries per lane instead of 35, the synthetic network 10 instead of 56)."""
+    from pycatkin_amd.functions.synthetic import synthetic_system
+
+    def evaluate(make, n, T, y, desc=None):
+        s = make()
+        plan = s.plan()
+        net = s.device()
+        Tt, p, d, fx, y0, inflow = s._inputs(net, plan, n, T, None, desc, None, None, None)
+        kf, kr = net.rate_constants(n, Tt, p, d)
+        f = net.species_rates(n, Tt, p, y, kf, kr, d, fx, inflow).cpu().numpy()
+        J = net.jacobian(n, Tt, p, y, kf, kr, d, fx, inflow).cpu().numpy()
+        return f, J
+
+    rng = np.random.default_rng(5)
+    cases = [(lambda: _ch4(P, inputs)[0], 8, np.linspace(450.0, 650.0, 8), rng.uniform(0.01, 1.0, (16, 8)), None)]
+    D = rng.uniform(-0.5, 0.5, (4, 6))
+    cases.append((lambda: synthetic_system()[0], 6, np.linspace(450.0, 650.0, 6), rng.uniform(0.0, 0.05, (50, 6)),
+                  {'D%d' % k: D[k] for k in range(4)}))
+    for make, n, T, y, desc in cases:
+        fb, Jb = evaluate(make, n, T, y, desc)
+        monkeypatch.setenv('PCK_GRP_BALANCE', '0')
+        fr, Jr = evaluate(make, n, T, y, desc)
+        monkeypatch.delenv('PCK_GRP_BALANCE')
+        np.testing.assert_allclose(fb, fr, rtol=1e-12, atol=1e-14 * np.abs(fr).max())
+        np.testing.assert_allclose(Jb, Jr, rtol=1e-12, atol=1e-14 * np.abs(Jr).max())
+    T = np.linspace(473.0, 573.0, 64)
+    a = _ch4(P, inputs, 1.0, 1.0)[0].solve_batch(T=T, t_end=1e4, rtol=1e-10, atol=1e-12, steady=True)
+    monkeypatch.setenv('PCK_GRP_BALANCE', '0')
+    b = _ch4(P, inputs, 1.0, 1.0)[0].solve_batch(T=T, t_end=1e4, rtol=1e-10, atol=1e-12, steady=True)
+    monkeypatch.delenv('PCK_GRP_BALANCE')
+    assert np.all(a['status'] == 0) and np.all(b['status'] == 0)
+    assert close(a['y'], b['y'], rtol=1e-9, floor=1e-15), np.abs(a['y'] - b['y']).max()
