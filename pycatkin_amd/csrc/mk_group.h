@@ -83,6 +83,12 @@ struct GrpView {
     const int32_t* xrows;
     int LS, NX, NXR;
 };
+// PCK_GRP_BAL: the balanced walk is decided at run time (-1, the compiled-in
+// kernels), compiled in (1) or out (0) (the hipRTC build knows the network)
+#ifndef PCK_GRP_BAL
+#define PCK_GRP_BAL -1
+#endif
+#define PCK_GRP_BAL_ON(g) (PCK_GRP_BAL == 1 || (PCK_GRP_BAL == -1 && (g).LS > 0))
 #define PCK_SCH_VALID 0x80000000u
 #define PCK_SCH_LAST 0x40000000u
 
@@ -375,7 +381,7 @@ __device__ __forceinline__ double grp_rhs(const GrpView& g, const Grp<NSP>& x, d
     for (int r = x.gl; r < x.R; r += G) x.d[r] = rec_rate(g.rx[r], x.kf[r], x.kr[r], x.c);
     wsync();
     double f = 0.0;
-    if (g.LS) {
+    if (PCK_GRP_BAL_ON(g)) {
         // balanced walk: every lane sums its pieces, the row's lane adds them up
         // the next word and its entry are fetched one iteration ahead (an
         // invalid word's entry index is 0: a harmless load)
@@ -465,7 +471,7 @@ __device__ __forceinline__ void grp_jac(const NetView& nv, const GrpView& g, con
     wsync();
     const double sc = sgn * x.rs;
     const double dg = shift - sgn * x.fl;
-    if (P == 1 && g.LS) {
+    if (P == 1 && PCK_GRP_BAL_ON(g)) {
         // balanced walk: each lane adds its pieces' terms into their rows (a
         // row's first piece into J, extras into Jx: every target row has one
         // writer), then the extras are folded into J per (row, column)
@@ -482,8 +488,10 @@ __device__ __forceinline__ void grp_jac(const NetView& nv, const GrpView& g, con
 #pragma unroll
                 for (int k = 0; k < PCK_GRP_NPMAX; ++k) {
                     if (k < np) {
+                        // one writer lane per target row: its LDS adds land in
+                        // program order (fire-and-forget ds_add, no read back)
                         const int sp = ent_species(q, k);
-                        dst[sp] += s * x.d[dp + k];
+                        atomicAdd(dst + sp, s * x.d[dp + k]);
                     }
                 }
             }

@@ -312,7 +312,7 @@ extern "C" int pck_network_create(const int32_t* ip, int64_t n_ip, const double*
         // balanced walk of the CSR (mk_group.h: GrpView::sch): rows longer than
         // K = ceil(NE / G) entries are cut into near-equal pieces, the pieces
         // packed onto the G lanes longest-first (least-loaded lane, lowest id on
-        // ties); taken when it shortens the longest walk (PCK_GRP_BALANCE=0: off)
+        // ties); PCK_GRP_BALANCE=0: off
         std::vector<uint32_t> sch;
         std::vector<int32_t> xbe(2 * (size_t)NS, 0), xrows;
         int LS = 0, NX = 0;
@@ -349,7 +349,12 @@ extern "C" int pck_network_create(const int32_t* ip, int64_t n_ip, const double*
                     load[l] += pcs[k].e - pcs[k].b;
                 }
                 for (int l = 0; l < G; ++l) LS = std::max(LS, load[l]);
-                if (LS >= net->grp_degmax || NS + NX > 1023) {
+                // taken where the longest row is at least 3x the balanced walk:
+                // the per-row rate loop takes two entries per iteration, and
+                // on CH4 (35 -> 17 entries) the balanced walk measured 1.5x
+                // slower per step; on the synthetic network (56 -> 10) 11 %
+                // faster (runs r3y / r3za)
+                if ((3 * LS > net->grp_degmax && !(eb && eb[0] == '2')) || NS + NX > 1023) {   // 2: always (tests)
                     LS = 0;                                 // no gain (or too many slots): the per-row loops
                 } else {
                     sch.assign((size_t)LS * G, 0u);
@@ -842,8 +847,9 @@ static int run_solver(const pck_network* net, const pck_conditions* cond, const 
         hipFunction_t f = nullptr;
         int P = grp_p(NS);
         int degmax = 0;
+        const int bal = net->gv.LS > 0 ? 1 : 0;
         if ((net->plan_mode != PCK_PLAN_RUNTIME || traj) && jit_enabled()) {
-            f = jit_group_kernel(NS, G, P, traj, false, net->grp_npmax, net->grp_emax, 0);
+            f = jit_group_kernel(NS, G, P, traj, false, net->grp_npmax, net->grp_emax, 0, bal);
             // uniform row loops bounded by the largest row degree (PCK_GRP_DEGMAX):
             // an A/B option (PCK_GRP_DEGMAX=1), taken only where they keep the
             // occupancy; measured slower (CH4 100.6 k -> 83.6 k solves/s, DMTM
@@ -851,7 +857,7 @@ static int run_solver(const pck_network* net, const pck_conditions* cond, const 
             const char* ev = getenv("PCK_GRP_DEGMAX");
             hipFunction_t fd = (f && ev && ev[0] == '1')
                                    ? jit_group_kernel(NS, G, P, traj, false, net->grp_npmax, net->grp_emax,
-                                                      net->grp_degmax)
+                                                      net->grp_degmax, bal)
                                    : nullptr;
             if (fd && grp_waves(fd) >= grp_waves(f)) { f = fd; degmax = net->grp_degmax; }
         }
@@ -862,8 +868,10 @@ static int run_solver(const pck_network* net, const pck_conditions* cond, const 
             if (rc) return rc;
             size_t shm_t;
             int qb_t;
-            if (grp_shape(net, NS, P, &shm_t, &qb_t, true) == PCK_OK && grp_tables_pay(f, shm, shm_t)) {
-                hipFunction_t ft = jit_group_kernel(NS, G, P, traj, true, net->grp_npmax, net->grp_emax, degmax);
+            const char* et = getenv("PCK_GRP_TAB");              // A/B: 0 = tables stay in global memory
+            if (!(et && et[0] == '0') && grp_shape(net, NS, P, &shm_t, &qb_t, true) == PCK_OK &&
+                grp_tables_pay(f, shm, shm_t)) {
+                hipFunction_t ft = jit_group_kernel(NS, G, P, traj, true, net->grp_npmax, net->grp_emax, degmax, bal);
                 if (ft) { f = ft; shm = shm_t; }
             }
             NetView nv = net->nv;

@@ -558,8 +558,9 @@ def test_balanced_walk_matches_row_loops(P, inputs, synthetic, monkeypatch):
     rows cut into pieces packed over the group's lanes) against the per-row
     loops it replaces (PCK_GRP_BALANCE=0 at network creation): the same sums
     in another order, so rates and Jacobians agree to rounding, and a CH4
-    steady solve lands on the same root.  Both networks use it (CH4 walks
-    17 entries per lane instead of 35, the synthetic network 10 instead of 56)."""
+    steady solve lands on the same root.  The synthetic network takes it
+    (10 entries per lane instead of 56); CH4 (17 vs 35) does not by default,
+    so its 'balanced' leg forces it (PCK_GRP_BALANCE=2)."""
     from pycatkin_amd.functions.synthetic import synthetic_system
 
     def evaluate(make, n, T, y, desc=None):
@@ -578,6 +579,7 @@ def test_balanced_walk_matches_row_loops(P, inputs, synthetic, monkeypatch):
     cases.append((lambda: synthetic_system()[0], 6, np.linspace(450.0, 650.0, 6), rng.uniform(0.0, 0.05, (50, 6)),
                   {'D%d' % k: D[k] for k in range(4)}))
     for make, n, T, y, desc in cases:
+        monkeypatch.setenv('PCK_GRP_BALANCE', '2')
         fb, Jb = evaluate(make, n, T, y, desc)
         monkeypatch.setenv('PCK_GRP_BALANCE', '0')
         fr, Jr = evaluate(make, n, T, y, desc)
@@ -585,6 +587,7 @@ def test_balanced_walk_matches_row_loops(P, inputs, synthetic, monkeypatch):
         np.testing.assert_allclose(fb, fr, rtol=1e-12, atol=1e-14 * np.abs(fr).max())
         np.testing.assert_allclose(Jb, Jr, rtol=1e-12, atol=1e-14 * np.abs(Jr).max())
     T = np.linspace(473.0, 573.0, 64)
+    monkeypatch.setenv('PCK_GRP_BALANCE', '2')
     a = _ch4(P, inputs, 1.0, 1.0)[0].solve_batch(T=T, t_end=1e4, rtol=1e-10, atol=1e-12, steady=True)
     monkeypatch.setenv('PCK_GRP_BALANCE', '0')
     b = _ch4(P, inputs, 1.0, 1.0)[0].solve_batch(T=T, t_end=1e4, rtol=1e-10, atol=1e-12, steady=True)
