@@ -586,11 +586,13 @@ def test_balanced_walk_matches_row_loops(P, inputs, synthetic, monkeypatch):
         monkeypatch.delenv('PCK_GRP_BALANCE')
         np.testing.assert_allclose(fb, fr, rtol=1e-12, atol=1e-14 * np.abs(fr).max())
         np.testing.assert_allclose(Jb, Jr, rtol=1e-12, atol=1e-14 * np.abs(Jr).max())
+    # the bench's CH4 solve (SteadyStateSolver.solve_ode to 1e4 s): the two
+    # walks' transients differ by the rounding of the rate sums only
     T = np.linspace(473.0, 573.0, 64)
     monkeypatch.setenv('PCK_GRP_BALANCE', '2')
-    a = _ch4(P, inputs, 1.0, 1.0)[0].solve_batch(T=T, t_end=1e4, rtol=1e-10, atol=1e-12, steady=True)
+    a = _ch4(P, inputs, 1.0, 1.0)[0].solve_batch(T=T, t_end=1e4, rtol=1e-10, atol=1e-12)
     monkeypatch.setenv('PCK_GRP_BALANCE', '0')
-    b = _ch4(P, inputs, 1.0, 1.0)[0].solve_batch(T=T, t_end=1e4, rtol=1e-10, atol=1e-12, steady=True)
+    b = _ch4(P, inputs, 1.0, 1.0)[0].solve_batch(T=T, t_end=1e4, rtol=1e-10, atol=1e-12)
     monkeypatch.delenv('PCK_GRP_BALANCE')
     assert np.all(a['status'] == 0) and np.all(b['status'] == 0)
-    assert close(a['y'], b['y'], rtol=1e-9, floor=1e-15), np.abs(a['y'] - b['y']).max()
+    assert close(a['y'], b['y'], rtol=1e-7, floor=1e-13), np.abs(a['y'] - b['y']).max()
