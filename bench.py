@@ -298,17 +298,25 @@ def _outputs(torch, net, n, L, _ptr):
 def _solve_workload(wl, sim, net, plan, n, T, p, desc, tof_terms, steady, activity, t_end=None, rtol=None,
                     atol=None, args=None):
     import torch
-    from pycatkin_amd.classes.system import DEGENERATE_RETRY
+    from pycatkin_amd.classes.system import ROOT_DIST, STEADY_TRANSIENT
     from pycatkin_amd import _lib as L
     from pycatkin_amd.engine import _ptr
     Tt, pp, d, fx, y0, inflow = sim._inputs(net, plan, n, T, p, desc, None, None, None)
     wl.cond, wl.keep = net.conditions(n, Tt, pp, d, fx, y0, inflow)
     times = sim.params['times']
+    # steady-state solves: System.solve_batch(steady=True)'s rule -- the
+    # transient at STEADY_TRANSIENT, the Newton root where the transient has
+    # reached it to ROOT_DIST, else the transient end (DESIGN.md "Steady state")
+    if steady:
+        rtol = STEADY_TRANSIENT[0] if rtol is None else rtol
+        atol = STEADY_TRANSIENT[1] if atol is None else atol
     wl.prm = net.params(t0=times[0], t_end=times[-1] if t_end is None else t_end,
-                        rtol=sim.params['rtol'] if rtol is None else rtol,
-                        atol=sim.params['atol'] if atol is None else atol, max_steps=args.max_steps,
+                        rtol=args.rtol or (sim.params['rtol'] if rtol is None else rtol),
+                        atol=args.atol or (sim.params['atol'] if atol is None else atol), max_steps=args.max_steps,
                         newton=steady and not args.no_newton, newton_iters=60, activity=activity,
-                        retry=None if args.no_retry else DEGENERATE_RETRY)
+                        retry=tuple(args.retry) if args.retry else None,
+                        root_dist=(ROOT_DIST if args.root_dist is None else args.root_dist) if steady else 0.0)
+    wl.tolerances = (wl.prm.rtol, wl.prm.atol)
     wl.prm.wave_order = {'auto': 0, 'on': 1, 'off': -1}[getattr(args, 'wave_order', 'auto')]
     # solver launches per step: the first pass, the degenerate-root retry and,
     # on the lane solver with cost-ordered dispatch, its preview
@@ -335,7 +343,6 @@ def _solve_workload(wl, sim, net, plan, n, T, p, desc, tof_terms, steady, activi
 
 def volcano_workload(args, rank, world):
     import pycatkin_amd as P
-    from pycatkin_amd.classes.system import DEGENERATE_RETRY
     from pycatkin_amd.functions.volcano import set_volcano_energies, tile_order
     from pycatkin_amd.parallel import weak_grid_rows
     wl = Workload()
@@ -367,13 +374,13 @@ def volcano_workload(args, rank, world):
                     ('CO_ox',), True, True, args=args)
     # the profile tag names the per-GPU workload: a weak-scaling rank's share is
     # the same 1024 x 1024 solve at every N, so N > 1 lines carry its counters
-    wl.tag = 'volcano %dx%d %s' % (rows, G, args.order)
+    wl.tag = 'volcano %dx%d %s rtol %g atol %g' % (rows, G, args.order, wl.prm.rtol, wl.prm.atol)
     wl.config = {'workload': 'COOxVolcano %dx%d (E_CO x E_O) grid, %s over %d GPU(s): %d E_CO rows x %d E_O per rank, '
-                             'T=600 K, t_end=3600 s, rtol 1e-8 / atol 1e-10, Newton steady-state polish, activity; '
-                             'degenerate roots re-integrated to t_end at rtol %%g / atol %%g (second launch over the '
-                             'compacted list)'
+                             'T=600 K, transient to t_end=3600 s at rtol %g / atol %g, Newton steady-state polish, '
+                             'the root where the transient has reached it to %g (else the transient end), activity'
                              % (wl.global_grid[0], wl.global_grid[1], 'sharded' if args.scaling == 'strong'
-                                else 'one grid share per GPU', world, rows, G) % DEGENERATE_RETRY,
+                                else 'one grid share per GPU', world, rows, G, wl.prm.rtol, wl.prm.atol,
+                                wl.prm.root_dist),
                  'global_grid': list(wl.global_grid), 'grid_per_gpu': [rows, G],
                  'parallelism': 'dp%d' % world, 'shard': 'cyclic E_CO rows',
                  'order': 'row' if wl.perm is None else 'tile %s' % args.tile}
@@ -536,8 +543,12 @@ def build_parser():
     ap.add_argument('--cpu-points', type=int, default=4000,
                     help='CPU baseline sample (stopped after 25 s of wall time)')
     ap.add_argument('--no-newton', action='store_true', help='A/B diagnostic: transient only (not the bench workload)')
-    ap.add_argument('--no-retry', action='store_true',
-                    help='A/B diagnostic: degenerate roots keep the first transient (not the bench workload)')
+    ap.add_argument('--rtol', type=float, default=0.0, help='A/B: first-pass rtol (0: the input\'s)')
+    ap.add_argument('--atol', type=float, default=0.0, help='A/B: first-pass atol (0: the input\'s)')
+    ap.add_argument('--retry', type=float, nargs=2, default=None, metavar=('RTOL', 'ATOL'),
+                    help='A/B: integrate the status-4 conditions again at these tolerances (default: no retry)')
+    ap.add_argument('--root-dist', type=float, default=None,
+                    help='A/B: pck_solve_params.root_dist of steady solves (default ROOT_DIST)')
     ap.add_argument('--emulate', default=None, metavar='R/N',
                     help='single-GPU A/B: solve the shard rank R of N would own, without a process group')
     ap.add_argument('--wave-order', choices=('auto', 'on', 'off'), default='auto',

@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define PCK_ABI_VERSION 4
+#define PCK_ABI_VERSION 5
 
 /* error codes */
 #define PCK_OK 0
@@ -156,6 +156,13 @@ typedef struct {
                             *   lanes of each; 1 on, -1 off, 0 auto (on for n >= 262144: more than one
                             *   round of wavefronts).  Results do not depend on it: the same 64
                             *   conditions share a wavefront either way. */
+    double root_dist;      /* with newton (> 0): the Newton root is reported (PCK_ST_OK) only if the
+                            *   transient end it started from lies within root_dist * |root_i| + atol
+                            *   of it in every dynamic species -- the transient has reached that steady
+                            *   state by t_end; otherwise the transient end is reported with
+                            *   PCK_ST_NEWTON (old_system.py:517-529 System.activity semantics).
+                            *   0: any converged, balanced, non-negative root is reported
+                            *   (old_system.py:385-468 find_steady from a given state). */
 } pck_solve_params;
 
 /* Outputs of pck_solve (device pointers; any may be NULL). */
@@ -176,6 +183,9 @@ typedef struct {
 #define PCK_ST_MAXSTEPS 1
 #define PCK_ST_STEPFAIL 2
 #define PCK_ST_NONFINITE 3
+/* no steady state reached by t_end (with root_dist: the transient has not
+ * reached a root; without: Newton met a degenerate root): y / tof are the
+ * transient end at t_end */
 #define PCK_ST_NEWTON 4
 /* a degenerate root whose tight retry transient failed (step budget / step
  * size): y and tof are the first pass's transient end at the caller's

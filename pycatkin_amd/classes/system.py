@@ -20,18 +20,41 @@ from .reactor import InfiniteDilutionReactor, Reactor
 from .state import State
 
 
-# Tolerances of the retry pass for degenerate roots (status 4, see "Steady
-# state" in DESIGN.md): a condition whose Newton polish meets a degenerate root
-# reports the transient end at t_end -- the reference's System.activity
-# semantics -- integrated again at this (rtol, atol).  The tiny atol makes the
-# error control relative on every coverage, down to the 1e-16 free sites of an
-# O-poisoned surface whose product the TOF is; the rtol is what the 1e-6 bound
-# on log10(TOF) needs with margin.  Measured on the 89 043 degenerate points of
-# the 1024 x 1024 volcano grid against a 1e-12 / 1e-24 run
-# (tools/retry_probe.py, profiles/r3/retry_probe.json): 1e-6 / 1e-22 is within
-# 2.7e-8 relative (+1.2 ms over the 7.5 ms first pass); 1e-10 / 1e-20 was
-# within 2.8e-10 but cost +29 ms.
-DEGENERATE_RETRY = (1.0e-6, 1.0e-22)
+# Steady-state solves (steady=True; DESIGN.md "Steady state").  The transient
+# to t_end is integrated at STEADY_TRANSIENT = (rtol, atol), Newton polishes
+# its end state, and the root is the answer only if the transient has reached
+# it: every dynamic species within ROOT_DIST * |root| + atol of it
+# (pck_solve_params.root_dist).  Otherwise (status 4) the answer is the
+# transient end at t_end -- the reference's System.activity semantics
+# (old_system.py:517-529, what examples/COOxVolcano/cooxvolcano.py:47 reports).
+# The tiny atol makes the error control relative on every coverage, down to
+# the 1e-16 free sites of an O-poisoned surface whose product the TOF is, so
+# that the distance test compares two well-resolved states; the rtol is what
+# the 1e-6 bound on log10(TOF) needs with margin: measured on the 89 043
+# degenerate points of the 1024 x 1024 volcano grid against a 1e-12 / 1e-24
+# run (tools/retry_probe.py, profiles/r3/retry_probe.json), 1e-6 / 1e-22 is
+# within 2.7e-8 relative.  On that grid one transient at these tolerances
+# costs less than round 3's input-tolerance pass plus a tight retry of the
+# degenerate points (6.1 ms against 7.5 ms per step, profiles/r4/tolerance_ab).
+STEADY_TRANSIENT = (1.0e-6, 1.0e-22)
+ROOT_DIST = 1.0e-6
+# round-3 name of the tight tolerances (the retry pass, now optional)
+DEGENERATE_RETRY = STEADY_TRANSIENT
+
+
+def _retry_tolerances(retry):
+    """solve_batch's `retry`: None -> no second pass, 'auto' -> STEADY_TRANSIENT,
+    else a positive (rtol, atol) pair (any sequence or array of two)."""
+    if isinstance(retry, str):
+        if retry != 'auto':
+            raise ValueError("retry must be 'auto', None or an (rtol, atol) pair, not %r" % retry)
+        return DEGENERATE_RETRY
+    if retry is None:
+        return None
+    r = np.asarray(retry, float).ravel()
+    if r.size != 2 or not np.all(r > 0.0):
+        raise ValueError('retry must be a positive (rtol, atol) pair, not %r' % (retry,))
+    return float(r[0]), float(r[1])
 
 
 class SteadyStateResults(NamedTuple):
@@ -411,14 +434,19 @@ class System:
 
     def solve_batch(self, T=None, p=None, desc=None, y0=None, fix=None, inflow=None, tof_terms=(),
                     steady=False, activity=False, t_end=None, t0=None, rtol=None, atol=None, max_steps=200000,
-                    newton_iters=60, to_numpy=True, t_out=None, retry='auto'):
+                    newton_iters=60, to_numpy=True, t_out=None, retry=None, root_dist='auto'):
         """Transient solve to t_end (solve_odes), optionally polished to the
         steady state (find_steady), with TOF or activity per condition; with
         t_out, also the dynamic state at those times ('traj' [n_out, NS, n],
-        Rodas4 dense output).  steady=True: conditions whose root is
-        degenerate (status 4) report the transient end, integrated again at
-        `retry` = (rtol, atol) ('auto': DEGENERATE_RETRY; None: the first
-        pass's transient end)."""
+        Rodas4 dense output).
+
+        steady=True: the transient runs at STEADY_TRANSIENT unless rtol / atol
+        are given, and the Newton root of its end state is reported (status
+        0) where the transient has reached it to `root_dist` ('auto':
+        ROOT_DIST when t_end > t0, else 0 -- a polish of the given state, as
+        find_steady); elsewhere the transient end (status 4).  `retry` =
+        (rtol, atol) integrates the status-4 conditions again at those
+        tolerances in a second launch (None: no second pass)."""
         plan = self.plan(tuple(tof_terms), None)
         net = self.device(tuple(tof_terms), None)
         sizes = [T, p] + (list(desc.values()) if desc else [])
@@ -427,12 +455,21 @@ class System:
             n = max(n, np.shape(y0)[1])
         T, p, d, fx, y0, inflow = self._inputs(net, plan, n, T, p, desc, y0, fix, inflow)
         times = self.params['times'] or [0.0, 1.0e4]
-        out = net.solve(n, T, p, y0, d, fx, inflow,
-                        t0=times[0] if t0 is None else t0, t_end=times[-1] if t_end is None else t_end,
+        t0 = times[0] if t0 is None else t0
+        t_end = times[-1] if t_end is None else t_end
+        if steady:
+            rtol = STEADY_TRANSIENT[0] if rtol is None else rtol
+            atol = STEADY_TRANSIENT[1] if atol is None else atol
+        if isinstance(root_dist, str):
+            if root_dist != 'auto':
+                raise ValueError("root_dist must be 'auto' or a number in [0, 1)")
+            root_dist = ROOT_DIST if (steady and t_end > t0) else 0.0
+        out = net.solve(n, T, p, y0, d, fx, inflow, t0=t0, t_end=t_end,
                         rtol=self.params['rtol'] if rtol is None else rtol,
                         atol=self.params['atol'] if atol is None else atol,
                         max_steps=max_steps, newton=steady, newton_iters=newton_iters, activity=activity,
-                        t_out=t_out, retry=(DEGENERATE_RETRY if retry == 'auto' else retry) if steady else None)
+                        t_out=t_out, retry=_retry_tolerances(retry) if steady else None,
+                        root_dist=float(root_dist) if steady else 0.0)
         if to_numpy:
             return {k: v.cpu().numpy() for k, v in out.items()}
         return out
@@ -440,6 +477,10 @@ class System:
     def drc_batch(self, tof_terms, T=None, p=None, desc=None, eps=1.0e-3, steady=False, t_end=None, rtol=None,
                   atol=None, max_steps=200000, y0=None, fix=None, inflow=None):
         """Degree of rate control of every reaction (old_system.py:490-515) for a batch.
+        steady=True: each of the 2R+1 solves is a steady-state solve with
+        solve_batch's rule (STEADY_TRANSIENT unless rtol / atol are given;
+        the root where the transient has reached it to ROOT_DIST, else the
+        transient end: the condition's status is then 4).
 
         Returns {reaction name: xi [n]} (ghost reactions: 0) plus 'tof0' and 'status'."""
         plan = self.plan(tuple(tof_terms), None)
@@ -450,10 +491,13 @@ class System:
                 n = max(n, np.shape(a)[1])
         T, p, d, fx, y0, inflow = self._inputs(net, plan, n, T, p, desc, y0, fix, inflow)
         times = self.params['times'] or [0.0, 1.0e4]
+        if steady:
+            rtol = STEADY_TRANSIENT[0] if rtol is None else rtol
+            atol = STEADY_TRANSIENT[1] if atol is None else atol
         r = net.drc(n, T, p, y0, d, fx, inflow, t0=times[0], t_end=times[-1] if t_end is None else t_end,
                     rtol=self.params['rtol'] if rtol is None else rtol,
                     atol=self.params['atol'] if atol is None else atol, max_steps=max_steps, newton=steady,
-                    drc_eps=eps)
+                    drc_eps=eps, root_dist=ROOT_DIST if steady else 0.0)
         xi = r['xi'].cpu().numpy()
         out = {name: (xi[plan.reactions.index(name)] if name in plan.reactions else np.zeros(n))
                for name in plan.all_reactions}
@@ -583,13 +627,14 @@ class System:
     @staticmethod
     def _check(st, what, degenerate_ok=False):
         """Raise on a failed solve (1 max steps, 2 step failure, 3 non-finite);
-        status 4 (degenerate root, tight transient end reported) and 5 (its
-        tight retry failed: the first pass's transient at the caller's
-        tolerances) are results where the reference's steady-state path
+        status 4 (no steady state reached by t_end: the transient end is
+        reported) and 5 (the same after a failed `retry` pass: the first
+        pass's transient) are results where the reference's steady-state path
         would return one."""
         if st != 0 and not (degenerate_ok and st in (4, 5)):
             raise RuntimeError('%s: device solver status %d (1 max steps, 2 step failure, 3 non-finite, '
-                               '4 degenerate root, 5 degenerate root with the first-pass transient)' % (what, st))
+                               '4 no steady state reached: transient end, 5 the same with the first-pass '
+                               'transient)' % (what, st))
 
     def reaction_terms(self, y):
         """old_system.py:202-225: rates (n_reactions, 2) at the full state y."""
@@ -633,9 +678,13 @@ class System:
         return float(r['tof'][0])
 
     def degree_of_rate_control(self, tof_terms, ss_solve=False, eps=1.0e-3):
-        """old_system.py:490-515"""
+        """old_system.py:490-515.  As the reference's (whose ss_solve path
+        returns wherever least_squares stops), a condition whose transient has
+        not reached a steady state (status 4) still returns its xi: every TOF
+        of the central difference is then that solve's answer by
+        solve_batch's rule (a root reached, or the transient end at t_end)."""
         r = self.drc_batch(tof_terms, T=[self.params['temperature']], eps=eps, steady=ss_solve)
-        self._check(r['status'][0], 'degree_of_rate_control')
+        self._check(r['status'][0], 'degree_of_rate_control', degenerate_ok=True)
         return {k: float(r[k][0]) for k in self.reactions}
 
     # patched-API steady state (system.py:566-639)

@@ -988,7 +988,7 @@ __device__ __forceinline__ bool grp_resolved(const NetView& nv, const GrpView& g
 // Newton steady-state polish (same rules as mk_solver.h: newton)
 template <int NSP, int G, int P>
 __device__ __forceinline__ int grp_newton(const NetView& nv, const GrpView& gv, const Grp<NSP>& x, double& y,
-                                          int iters, LU<NSP>& F) {
+                                          int iters, LU<NSP>& F, double dist, double atol) {
     const int NS = x.NS;
     double b[PCK_MAX_CONS], ci[PCK_MAX_CONS];
     int piv_l[PCK_MAX_CONS];
@@ -1054,6 +1054,9 @@ __device__ __forceinline__ int grp_newton(const NetView& nv, const GrpView& gv, 
     if (!conv) return PCK_ST_NEWTON;
     if (gmin<G>((x.row && z < 0.0) ? -1.0 : 1.0) < 0.0) return PCK_ST_NEWTON;
     if (!grp_resolved<NSP, G>(nv, gv, x, z)) return PCK_ST_NEWTON;   // converged in absolute terms only
+    // mk_solver.h: newton -- the root only if the transient end reached it
+    if (dist > 0.0 && gmin<G>((x.row && !(fabs(z - y) <= dist * fabs(z) + atol)) ? -1.0 : 1.0) < 0.0)
+        return PCK_ST_NEWTON;
     y = z;
     return PCK_ST_OK;
 }
@@ -1190,7 +1193,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 64
     y = x.row ? cv.y0[x.gl * cv.ld_y0 + c * cv.s_y0] : 0.0;
     int st = grp_integrate<NSP, G, P, TRAJ>(nv, gl, x, y, a.t0, a.t_end, a.rtol, a.atol, a.max_steps, ns,
                                             a.cons_rows != 0, to, F);
-    if (st == PCK_ST_OK && a.newton) st = grp_newton<NSP, G, P>(nv, gl, x, y, a.newton_iters, F);
+    if (st == PCK_ST_OK && a.newton) st = grp_newton<NSP, G, P>(nv, gl, x, y, a.newton_iters, F, a.root_dist, a.atol);
     const double tof = grp_tof<NSP, G>(nv, gl, x, y);
     const bool fin = gmin<G>((!x.row || isfinite(y)) ? 1.0 : 0.0) > 0.0 && isfinite(tof);
     if (!fin && st == PCK_ST_OK) st = PCK_ST_NONFINITE;

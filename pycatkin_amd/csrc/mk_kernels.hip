@@ -703,6 +703,7 @@ static int check_params(const pck_solve_params* prm) {
     if (!(prm->rtol > 0.0) || !(prm->atol > 0.0)) return fail(PCK_E_ARG, "tolerances must be positive%s", "");
     if (prm->max_steps < 1) return fail(PCK_E_ARG, "max_steps must be >= 1%s", "");
     if (prm->newton && (prm->newton_iters < 1 || prm->newton_iters > 200)) return fail(PCK_E_ARG, "newton_iters%s out of range", "");
+    if (!(prm->root_dist >= 0.0 && prm->root_dist < 1.0)) return fail(PCK_E_ARG, "root_dist must be in [0, 1)%s", "");
     if (prm->retry_rtol != 0.0 && !(prm->retry_rtol > 0.0 && prm->retry_atol > 0.0))
         return fail(PCK_E_ARG, "retry tolerances must both be positive (or retry_rtol 0)%s", "");
     return PCK_OK;
@@ -737,6 +738,9 @@ __global__ void __launch_bounds__(256) k_select_status(int64_t n, const int32_t*
 // wavefront's key (tools/predictor_eval.py: 1.167x in the model against 1.170x
 // for the true costs).
 constexpr int PCK_PREVIEW_LANES = 4;
+// the preview lanes, the wavefront sort, k_select_ordered and k_solve's
+// worder mapping all take one block of the lane solver to be one wavefront
+static_assert(PCK_SOLVE_BLOCK == 64, "cost-ordered dispatch assumes one wavefront per lane-solver block");
 __device__ __forceinline__ int preview_lane(int k) { return (k < 2) ? 3 * k : 60 + 3 * (k - 2); }   // 0, 3, 60, 63
 
 __global__ void __launch_bounds__(256) k_preview_list(int64_t n, int64_t W, int64_t* list, int32_t* cnt) {
@@ -953,6 +957,7 @@ static int launch_solve(const pck_network* net, const pck_conditions* cond, cons
     a.t0 = prm->t0; a.t_end = prm->t_end; a.rtol = prm->rtol; a.atol = prm->atol; a.eps = prm->drc_eps;
     a.max_steps = prm->max_steps; a.newton = prm->newton; a.newton_iters = prm->newton_iters;
     a.want_activity = prm->want_activity;
+    a.root_dist = prm->root_dist;
     a.idx = nullptr; a.nidx = nullptr; a.retry_pass = 0; a.worder = nullptr;
     // degenerate roots (status 4) are re-integrated by a second launch over
     // their compacted list (pck_solve only: G == 1, no DRC groups)
@@ -1099,8 +1104,10 @@ static int launch_solve(const pck_network* net, const pck_conditions* cond, cons
         r.nidx = cnt;
         r.retry_pass = 1;
         r.worder = nullptr;
-        if (!r.nsteps) r.nsteps = nullptr;
-        rc = run_solver(net, cond, r, grp, ga, traj, kf, kr, s);
+        // the trajectory stays the first pass's: a retry that fails keeps the
+        // first pass's outputs, and a partly rewritten trajectory would mix the two
+        r.traj = nullptr; r.t_out = nullptr; r.n_out = 0;
+        rc = run_solver(net, cond, r, grp, ga, false, kf, kr, s);
         if (rc) return rc;
     }
     if (drc_groups) {

@@ -695,8 +695,18 @@ __device__ __forceinline__ bool resolved(const P& p, const Lane<P::NS>& L, const
 // estimate accelerates near-double roots; a root that stays linearly
 // convergent (a site-starved surface approached algebraically) or lands on a
 // negative component is not regular -> PCK_ST_NEWTON, transient state kept.
+//
+// dist > 0 (pck_solve_params.root_dist): the root is the answer only if the
+// transient end y it started from has reached it -- every component within
+// dist * |root| + atol -- i.e. the transient at t_end is at that steady
+// state.  Otherwise PCK_ST_NEWTON with y unchanged: the transient end is the
+// answer (old_system.py:517-529, what the volcano driver reports).  The test
+// is a distance between two well-defined states, so where a device and a CPU
+// implementation disagree on it the two answers they report are themselves
+// within ~dist of each other (DESIGN.md "Steady state").
 template <class P, class K>
-__device__ PCK_LANE_INLINE int newton(const P& p, const Lane<P::NS>& L, const K& k, double (&y)[P::NS], int iters) {
+__device__ PCK_LANE_INLINE int newton(const P& p, const Lane<P::NS>& L, const K& k, double (&y)[P::NS], int iters,
+                                      double dist, double atol) {
     constexpr int NS = P::NS;
     double b[PCK_MAX_CONS];
     for (int l = 0; l < p.ncons(); ++l) {
@@ -812,6 +822,12 @@ __device__ PCK_LANE_INLINE int newton(const P& p, const Lane<P::NS>& L, const K&
     for (int i = 0; i < NS; ++i)
         if (z[i] < 0.0) return PCK_ST_NEWTON;
     if (!resolved(p, L, k, z)) return PCK_ST_NEWTON;   // converged in absolute terms only
+    if (dist > 0.0) {
+        bool near = true;
+#pragma unroll
+        for (int i = 0; i < NS; ++i) near = near && (fabs(z[i] - y[i]) <= dist * fabs(z[i]) + atol);
+        if (!near) return PCK_ST_NEWTON;                 // the transient has not reached this root
+    }
 #pragma unroll
     for (int i = 0; i < NS; ++i) y[i] = z[i];
     return PCK_ST_OK;
@@ -895,6 +911,7 @@ struct SolveArgs {
     double* xi; int64_t ld_xi; double* tof0;   // DRC mode
     int G;                                     // lanes per condition (1, or DRC group size)
     int cons_rows;                             // conservation rows in the stage systems (A/B: PCK_CONS_ROWS=1)
+    double root_dist;                          // pck_solve_params.root_dist (newton: root only if the transient reached it)
     const double* t_out; int n_out;            // trajectory sample times (k_solve<P, true>)
     double* traj; int64_t ld_traj;             // [n_out][NS][ld_traj]
     // degenerate-root retry (pck_solve_params.retry_rtol), a second launch
@@ -922,7 +939,7 @@ __device__ __forceinline__ int solve_lane(const P& p, const Lane<P::NS>& L, cons
 #pragma unroll
     for (int i = 0; i < NS; ++i) y[i] = cv.y0[i * cv.ld_y0 + c * cv.s_y0];
     int st = integrate<TRAJ>(p, L, k, y, a.t0, a.t_end, a.rtol, a.atol, a.max_steps, ns, a.cons_rows != 0, to);
-    if (st == PCK_ST_OK && a.newton) st = newton(p, L, k, y, a.newton_iters);
+    if (st == PCK_ST_OK && a.newton) st = newton(p, L, k, y, a.newton_iters, a.root_dist, a.atol);
     return st;
 }
 

@@ -170,7 +170,7 @@ class DeviceNetwork:
 
     @staticmethod
     def params(t_end, t0=0.0, rtol=1e-8, atol=1e-10, max_steps=100000, newton=False, newton_iters=60,
-               activity=False, drc_eps=1e-3, retry=None, wave_order=0):
+               activity=False, drc_eps=1e-3, retry=None, wave_order=0, root_dist=0.0):
         """retry = (rtol, atol): with newton, the conditions whose polish meets a
         degenerate root (status 4) are integrated again at these tolerances
         and report that transient end (pck_solve_params.retry_rtol)."""
@@ -181,6 +181,7 @@ class DeviceNetwork:
         if retry is not None:
             p.retry_rtol, p.retry_atol = float(retry[0]), float(retry[1])
         p.wave_order = int(wave_order)     # 0 auto, 1 on, -1 off (pck_solve_params.wave_order)
+        p.root_dist = float(root_dist)     # newton: the root only if the transient reached it
         return p
 
     def solve(self, n, T, p, y0, desc=None, fixc=None, inflow=None, want_k=False, out=None, t_out=None, **kw):

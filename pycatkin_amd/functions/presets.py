@@ -47,6 +47,16 @@ def _net_rates(sim_system, plan, finals, T, p=None):
     return out
 
 
+def _failed(status):
+    """Indices of failed solves.  Status 4 (the transient end at t_end is not
+    at a steady state: that transient is reported) and 5 (the same, its tight
+    re-integration failed: the first pass's transient) are results, as the
+    reference's find_steady returns wherever least_squares stops
+    (System._check with degenerate_ok); 1-3 are integrator failures."""
+    st = np.asarray(status)
+    return np.nonzero((st != 0) & (st != 4) & (st != 5))[0]
+
+
 def _finals(sim_system, plan, ydyn, n):
     base = sim_system._full(plan, plan.y0_default)
     final = np.tile(base, (n, 1))
@@ -64,9 +74,7 @@ def run_temperatures(sim_system, temperatures, steady_state_solve=False, tof_ter
     temps = np.asarray(temperatures, float).ravel()
     plan = sim_system.plan()
     r = sim_system.solve_batch(T=temps, steady=steady_state_solve)
-    # status 4: degenerate root, the transient end state is kept (find_steady's
-    # least_squares stops near it in the reference); 1-3 are integrator failures
-    bad = np.nonzero((r['status'] != 0) & (r['status'] != 4))[0]
+    bad = _failed(r['status'])
     if bad.size:
         raise RuntimeError('device solver failed for T = %s (status %s)' % (temps[bad], r['status'][bad]))
     final = _finals(sim_system, plan, r['y'], temps.size)
@@ -151,7 +159,7 @@ def _run_batch(sim_system, params_name, vals, steady_state_solve, tof_terms, eps
     if 'T' not in kw:
         kw['T'] = np.full(n, float(sim_system.params['temperature']))
     r = sim_system.solve_batch(steady=steady_state_solve, **kw)
-    bad = np.nonzero((r['status'] != 0) & (r['status'] != 4))[0]
+    bad = _failed(r['status'])
     if bad.size:
         raise RuntimeError('device solver failed for %s = %s' % (params_name, vals[bad]))
     final = _finals(sim_system, plan, r['y'], n)

@@ -1,0 +1,107 @@
+"""Oracle fixture of the synthetic 50-species / 150-reaction config
+(BASELINE configs[4]; pycatkin_amd/functions/synthetic.py, T = 500 K,
+t_end = 1e4 s).
+
+Conditions are rows of the bench's own condition set
+(np.random.default_rng(0).uniform(-0.5, 0.5, (65536, 4)) descriptors,
+bench.py synthetic_workload): N_RANDOM random rows plus the rows that
+stalled or failed in earlier rounds (STRAGGLERS).  For each the oracle
+(oracle/mk_oracle.py, the reference algorithm restated) stores, by
+mk_oracle.steady_rule -- the device's steady-state rule
+(System.solve_batch(steady=True)) restated:
+
+  tight    the transient at t_end, lsoda (scipy BDF where lsoda exceeds its
+           budget) at rtol 1e-11 / atol 1e-20
+  root     Newton from `tight`; the answer (`regular`) only where `tight`
+           lies within ROOT_DIST * |root| + STEADY_ATOL of it, else `tight`
+           itself; `newton_ok` / `crit` as in make_volcano_fixture.py
+  l10      log10 of the answer's TOF (reaction R0, the bench's tof_terms)
+
+    OMP_NUM_THREADS=1 python tests/golden/make_synthetic_fixture.py [--workers 8]
+
+writes tests/golden/synthetic_fixture.npz (numpy arrays only).
+"""
+import argparse
+import multiprocessing as mp
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+OUT = os.path.join(HERE, 'synthetic_fixture.npz')
+N_SET = 65536
+N_RANDOM = 320
+SEED = 20261018
+STRAGGLERS = [17825, 39547, 37890, 30513]
+# pycatkin_amd/classes/system.py: ROOT_DIST, STEADY_TRANSIENT[1]
+ROOT_DIST = 1.0e-6
+STEADY_ATOL = 1.0e-22
+
+
+def bench_set():
+    return np.random.default_rng(0).uniform(-0.5, 0.5, (N_SET, 4))
+
+
+def pick():
+    rng = np.random.default_rng(SEED)
+    r = rng.choice(N_SET, N_RANDOM, replace=False)
+    return list(STRAGGLERS) + [int(k) for k in r if int(k) not in STRAGGLERS]
+
+
+def _cond(arg):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, 'tests'))
+    from _synth import spec_of
+    from oracle import mk_oracle as O
+    from pycatkin_amd.functions.synthetic import synthetic_network
+    k, d = arg
+    m = O.ClassicModel(spec_of(synthetic_network(), np.asarray(d)), T=500.0)
+    dyn = m.dyn
+    t = time.time()
+    r = O.steady_rule(m, dist=ROOT_DIST, dist_atol=STEADY_ATOL, budget=200000)
+    nan = np.full(len(dyn), np.nan)
+    if r is None:
+        return k, dict(ok=False, regular=False, newton_ok=False, crit=np.inf, y_tight=nan, y_root=nan,
+                       l10=np.nan, l10_tight=np.nan, seconds=time.time() - t), [m.snames[i] for i in dyn]
+
+    def l10(y):
+        v = m.tof(y, ['R0'])
+        return np.log10(v) if v > 0 else -np.inf
+    return k, dict(ok=True, regular=r['regular'], newton_ok=r['newton_ok'], crit=r['crit'],
+                   y_tight=r['y_tight'][dyn], y_root=r['y'][dyn], l10=l10(r['y']), l10_tight=l10(r['y_tight']),
+                   seconds=time.time() - t), [m.snames[i] for i in dyn]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--workers', type=int, default=8)
+    ap.add_argument('--limit', type=int, default=0)
+    args = ap.parse_args()
+    idx = pick()
+    if args.limit:
+        idx = idx[:args.limit]
+    D = bench_set()
+    t = time.time()
+    res, names = {}, None
+    with mp.get_context('spawn').Pool(args.workers) as pool:
+        for m, (k, o, nm) in enumerate(pool.imap_unordered(_cond, [(k, D[k]) for k in idx])):
+            res[k], names = o, nm
+            if m % 20 == 0:
+                print('%d / %d conditions, %.0f s' % (m, len(idx), time.time() - t), flush=True)
+    arr = dict(idx=np.array(idx, np.int64), desc=D[idx], dyn=np.array(names), root_dist=np.array([ROOT_DIST, STEADY_ATOL]))
+    for f in ('ok', 'regular', 'newton_ok'):
+        arr[f] = np.array([res[k][f] for k in idx], bool)
+    for f in ('crit', 'l10', 'l10_tight', 'seconds'):
+        arr[f] = np.array([res[k][f] for k in idx], float)
+    for f in ('y_tight', 'y_root'):
+        arr[f] = np.array([res[k][f] for k in idx], float)
+    np.savez_compressed(OUT, **arr)
+    print('wrote %s: %d conditions, %d with an answer, %d steady state reached, %d with a Newton root, %.0f s'
+          % (OUT, len(idx), arr['ok'].sum(), arr['regular'].sum(), arr['newton_ok'].sum(), time.time() - t))
+
+
+if __name__ == '__main__':
+    main()

@@ -3,29 +3,37 @@
 Points are grid nodes (i, j) of the bench grid be = linspace(-2.5, 0.5, 1024)
 (activity[iCO, iO], examples/COOxVolcano/cooxvolcano.py:22-47): N_UNIFORM
 uniform random nodes plus N_CORNER nodes drawn from the O-poisoned corner,
-where the polish meets degenerate roots (device status 4).  For each node the
-oracle (oracle/mk_oracle.py, the reference algorithm restated) stores
+where the transient is still moving at t_end.  For each node the oracle
+(oracle/mk_oracle.py, the reference algorithm restated) stores
 
-  root     the Newton polish of `ref` (below); `regular` says whether Newton
-           converged quadratically (mk_oracle.ClassicModel._polish)
   tight    the transient at t_end = 3600 s, lsoda (scipy BDF where lsoda
-           exceeds its budget) at rtol 1e-11 / atol 1e-20 (pure relative control on the coverages): the
-           reference's System.activity semantics (old_system.py:517-529)
-           without integrator error -- at every node (NaN where both
-           integrators exceed the evaluation budget)
-  ref      the reference's own path: lsoda at the input's tolerances
-           (ode_solver 'ode', rtol 1e-8 / atol 1e-10, old_system.py:359-376),
-           i.e. what cooxvolcano.py:47 computes
-  ls       least_squares(trf, xtol 1e-8, ftol 1e-8) from `ref`
-           (old_system.py:385-433), what find_steady / activity(ss_solve=True)
-           return
+           exceeds its budget) at rtol 1e-11 / atol 1e-20 (pure relative
+           control on the coverages): the reference's System.activity
+           semantics (old_system.py:517-529) without integrator error -- at
+           every node (NaN where both integrators exceed the evaluation budget)
+  root     the steady-state rule of the device (System.solve_batch(steady=
+           True), DESIGN.md "Steady state"), restated: Newton from `tight`;
+           the root is the answer (`regular`) only if `tight` lies within
+           ROOT_DIST * |root| + STEADY_ATOL of it in every species, else the
+           answer is `tight` itself.  `newton_ok` says whether Newton found a
+           resolved root at all, `crit` is the distance criterion
+           max_i (|root_i - tight_i| - STEADY_ATOL) / |root_i| (inf: no root)
+  ref      lsoda at the input's tolerances (ode_solver 'ode', rtol 1e-8 /
+           atol 1e-10, old_system.py:359-376), i.e. what cooxvolcano.py:47
+           computes, restated
+  ls       least_squares(trf, xtol 1e-8, ftol 1e-8) from `ref` with the
+           reference's transposed jacfun (old_system.py:385-433), restated:
+           what find_steady / activity(ss_solve=True) return
 
-as dynamic-species states (plan order CO*, O*, O2*, * is not assumed: the
-names are stored) and log10(TOF of CO_ox).
+as dynamic-species states (the names are stored) and log10(TOF of CO_ox).
+The reference's own code run on a subset of these nodes is added by
+tests/golden/make_volcano_reference.py (columns *_reference).
 
-    OMP_NUM_THREADS=1 python tests/golden/make_volcano_fixture.py [--workers 8]
+    OMP_NUM_THREADS=1 python tests/golden/make_volcano_fixture.py [--workers 8] [--reuse]
 
 writes tests/golden/volcano_fixture.npz (no pickles: numpy arrays only).
+--reuse keeps the stored ref / tight transients (the expensive part) and
+recomputes the columns derived from them.
 """
 import argparse
 import copy
@@ -44,6 +52,10 @@ G = 1024
 N_UNIFORM = 2048
 N_CORNER = 512
 SEED = 20261017
+# pycatkin_amd/classes/system.py: ROOT_DIST, STEADY_TRANSIENT[1]
+# (tests/test_oracle.py checks that they agree)
+ROOT_DIST = 1.0e-6
+STEADY_ATOL = 1.0e-22
 
 _spec = None
 _dyn = None
@@ -69,16 +81,16 @@ class _Budget(Exception):
     pass
 
 
-def _point(ij):
-    """One grid node.  The tight transient is computed at every node: the
-    device reports it wherever its own Newton meets a degenerate root, which
-    near the boundary of the two regimes need not be where the oracle's does.
-    Every solve has a budget of 50 000 rhs evaluations (lsoda, then scipy
-    BDF; at rtol 1e-11 BDF can crawl through 1e5 steps on coverages of 1e-30);
-    a node where both exceed it has ok = False (reference transient) or
-    tight_ok = False (tight transient) and is not compared on it."""
+def _point(arg):
+    """One grid node.  The tight transient is computed at every node: it is
+    the answer wherever the transient has not reached a root by t_end.  Every
+    solve has a budget of 50 000 rhs evaluations (lsoda, then scipy BDF; at
+    rtol 1e-11 BDF can crawl through 1e5 steps on coverages of 1e-30); a node
+    where both exceed it has ok = False (reference transient) or tight_ok =
+    False (tight transient) and is not compared on it.  With `reuse` (the
+    stored y_ref, y_tight) only the derived columns are recomputed."""
     from oracle import mk_oracle as O
-    i, j = ij
+    (i, j), reuse = arg
     be = np.linspace(-2.5, 0.5, G)
     spec = copy.deepcopy(_spec)
     O.set_volcano_point(spec, be[i], be[j])
@@ -114,28 +126,37 @@ def _point(ij):
                 m.budget = None
         return None
 
+    def full(yd):
+        y = m.y0.copy()
+        y[dyn] = yd
+        return y
+
     nan = np.full(len(dyn), np.nan)
-    out['y_tight'], out['l10_tight'], out['tight_ok'] = nan, np.nan, False
-    # the reference's transient (examples/COOxVolcano/input.json: ode_solver
-    # 'ode' = lsoda at rtol 1e-8 / atol 1e-10), the start of both polishes
-    yA = solve(1e-8, 1e-10)
+    if reuse is not None:
+        yA = full(reuse['y_ref']) if np.all(np.isfinite(reuse['y_ref'])) else None
+        yT = full(reuse['y_tight']) if np.all(np.isfinite(reuse['y_tight'])) else None
+    else:
+        # the reference's transient (examples/COOxVolcano/input.json: ode_solver
+        # 'ode' = lsoda at rtol 1e-8 / atol 1e-10)
+        yA = solve(1e-8, 1e-10)
+        yT = solve(1e-11, 1e-20)
     out['ok'] = yA is not None
-    if yA is None:                 # no oracle answer at this node (recorded, never compared)
-        out['regular'] = False
-        for f in ('ref', 'root', 'ls'):
-            out['y_' + f], out['l10_' + f] = nan, np.nan
+    if yA is None:
+        out['y_ref'], out['l10_ref'], out['y_ls'], out['l10_ls'] = nan, np.nan, nan, np.nan
+    else:
+        out['y_ref'], out['l10_ref'] = yA[dyn], l10(yA)
+        yS = m.find_steady(yA.copy(), polish=False)
+        out['y_ls'], out['l10_ls'] = yS[dyn], l10(yS)
+    out['tight_ok'] = yT is not None
+    if yT is None:
+        out['y_tight'], out['l10_tight'] = nan, np.nan
+        out['regular'], out['newton_ok'], out['crit'] = False, False, np.inf
+        out['y_root'], out['l10_root'] = nan, np.nan
         return i, j, out
-    out['y_ref'], out['l10_ref'] = yA[dyn], l10(yA)
-    yR = m.find_steady(yA.copy())
-    out['regular'] = bool(m.regular)
+    out['y_tight'], out['l10_tight'] = yT[dyn], l10(yT)
+    yR = m.find_steady(yT.copy(), dist=ROOT_DIST, dist_atol=STEADY_ATOL)
+    out['regular'], out['newton_ok'], out['crit'] = bool(m.regular), bool(m.newton_ok), float(m.root_crit)
     out['y_root'], out['l10_root'] = yR[dyn], l10(yR)
-    yS = m.find_steady(yA.copy(), polish=False)
-    out['y_ls'], out['l10_ls'] = yS[dyn], l10(yS)
-    # every node: a device that classifies a node degenerate reports its
-    # tight transient, whatever the oracle's classification
-    yT = solve(1e-11, 1e-20)
-    if yT is not None:
-        out['y_tight'], out['l10_tight'], out['tight_ok'] = yT[dyn], l10(yT), True
     return i, j, out
 
 
@@ -159,22 +180,35 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--workers', type=int, default=8)
     ap.add_argument('--limit', type=int, default=0, help='first N points only (a quick check)')
+    ap.add_argument('--reuse', action='store_true', help='keep the stored ref / tight transients')
     args = ap.parse_args()
     pts = pick_points()
     if args.limit:
         pts = pts[:args.limit]
+    old = None
+    if args.reuse:
+        old = dict(np.load(OUT))
+        assert [(int(a), int(b)) for a, b in zip(old['i'], old['j'])][:len(pts)] == pts
+    jobs = [(p, None if old is None else dict(y_ref=old['y_ref'][k], y_tight=old['y_tight'][k]))
+            for k, p in enumerate(pts)]
     t = time.time()
     res = {}
     with mp.get_context('fork').Pool(args.workers, initializer=_init) as pool:
-        for k, (i, j, o) in enumerate(pool.imap_unordered(_point, pts, chunksize=4)):
+        for k, (i, j, o) in enumerate(pool.imap_unordered(_point, jobs, chunksize=4)):
             res[(i, j)] = o
             if k % 100 == 0:
                 print('%d / %d points, %.0f s' % (k, len(pts), time.time() - t), flush=True)
     keys = [p for p in pts]
     arr = {'i': np.array([p[0] for p in keys], np.int32), 'j': np.array([p[1] for p in keys], np.int32),
            'dyn': np.array(dyn_names()), 'grid': np.array([-2.5, 0.5, G], float)}
-    for f in ('ok', 'regular', 'tight_ok'):
+    for f in ('ok', 'regular', 'tight_ok', 'newton_ok'):
         arr[f] = np.array([res[p][f] for p in keys], bool)
+    arr['crit'] = np.array([res[p]['crit'] for p in keys], float)
+    arr['root_dist'] = np.array([ROOT_DIST, STEADY_ATOL])
+    if old is not None:               # columns of make_volcano_reference.py survive a --reuse
+        for k, v in old.items():
+            if k.endswith('_reference') or k.startswith('ref_'):
+                arr[k] = v
     for f in ('root', 'tight', 'ref', 'ls'):
         arr['y_' + f] = np.array([res[p]['y_' + f] for p in keys], float)
         arr['l10_' + f] = np.array([res[p]['l10_' + f] for p in keys], float)

@@ -48,23 +48,30 @@ RTOL = 1e-6
 
 def test_volcano_fixture_parity(P, inputs):
     """Every node of tests/golden/volcano_fixture.npz solved as the bench
-    solves it (transient at the input's rtol 1e-8 / atol 1e-10, Newton polish,
-    degenerate roots re-integrated at DEGENERATE_RETRY):
+    solves it (System.solve_batch(steady=True): the transient to t_end =
+    3600 s at STEADY_TRANSIENT, Newton from its end, the root reported where
+    the transient has reached it to ROOT_DIST, else the transient end), against
+    the oracle's restatement of the same rule from its tight transient (lsoda,
+    rtol 1e-11 / atol 1e-20; make_volcano_fixture.py):
 
-    * status 0 (regular root): coverages and log10(TOF) within 1e-6 relative
-      of the oracle's polished root (coverage floor 1e-15);
-    * status 4 (degenerate root, the O-poisoned corner): the reported state is
-      the transient end at t_end = 3600 s, the reference's System.activity
-      semantics (cooxvolcano.py:47): log10(TOF) within 1e-6 relative of the
-      oracle's tight transient (lsoda, rtol 1e-11 / atol 1e-20), and every
-      coverage within 1e-6 relative of it;
-    * the regular / degenerate classification agrees with the oracle's on all
-      but a stated handful of nodes on the boundary of the two regimes, and
-      those still meet the bound of the semantics the device reports.
-    The reference's own numbers are reported next to these (not asserted):
-    its lsoda transient at 1e-8 / 1e-10 and least_squares' answer from it."""
+    * every node, whatever either side's classification: log10(TOF) within
+      1e-6 relative of the oracle's answer (the rule makes the answer
+      classification-independent: where the two sides classify a node
+      differently, both answers lie within ~ROOT_DIST of the transient end);
+    * nodes both sides call regular (status 0): coverages within 1e-6
+      relative of the oracle's root (floor 1e-15); nodes both call
+      "not reached" (status 4): within 1e-6 of the tight transient (floor
+      1e-20, its atol);
+    * the classification differs on at most 1 % of the nodes (0.2 % of the
+      uniform ones), and only where the oracle's criterion lies within a
+      factor 2 of ROOT_DIST -- the integrators' own error (~1e-7) moving it
+      across the threshold.  There the coverages agree to 2 * ROOT_DIST.
+    The reference's own numbers are reported next to these (not asserted
+    here): its lsoda transient at 1e-8 / 1e-10 and least_squares' answer."""
+    from pycatkin_amd.classes.system import ROOT_DIST, STEADY_TRANSIENT
     from pycatkin_amd.functions.volcano import set_volcano_energies
-    fx = np.load(os.path.join(GOLDEN, 'volcano_fixture.npz'))
+    fx = dict(np.load(os.path.join(GOLDEN, 'volcano_fixture.npz')))
+    assert tuple(fx['root_dist']) == (ROOT_DIST, STEADY_TRANSIENT[1])
     lo, hi, G = fx['grid']
     be = np.linspace(lo, hi, int(G))
     eco, eo = be[fx['i']], be[fx['j']]
@@ -80,107 +87,63 @@ def test_volcano_fixture_parity(P, inputs):
     l10 = np.log10(r['tof'])
     dev_reg = st == 0
     reg = fx['regular']
+    ok = fx['tight_ok']                       # nodes with an oracle answer (12 of 2 560 exceed its budget)
 
-    def rel_l10(a, b):
+    def rel(a, b):
         return np.abs(a - b) / np.maximum(np.abs(b), 1e-300)
 
-    both = dev_reg & reg
-    err_root = rel_l10(l10[both], fx['l10_root'][both])
-    cov_root = np.abs(y[both] - fx['y_root'][both]) <= RTOL * np.abs(fx['y_root'][both]) + 1e-15
-    deg = ~dev_reg
-    # the transient end at t_end: the tight oracle transient, or -- at a regular
-    # node whose transient had settled onto its root -- that root
-    l10_t = np.where(fx['tight_ok'], fx['l10_tight'], fx['l10_root'])
-    y_t = np.where(fx['tight_ok'][:, None], fx['y_tight'], fx['y_root'])
-    assert np.all(fx['tight_ok'][deg] | reg[deg])
-    err_tight = rel_l10(l10[deg], l10_t[deg])
-    # coverages: 1e-6 relative above the tight oracle's own absolute accuracy
-    # (its atol 1e-20: a coverage below that is not resolved by the reference
-    # transient either)
-    cov_tight = np.abs(y[deg] - y_t[deg]) <= RTOL * np.abs(y_t[deg]) + 1e-20
-    flips = np.nonzero(dev_reg != reg)[0]
-    info = dict(n=int(n), n_regular=int(dev_reg.sum()), n_degenerate=int(deg.sum()), n_flips=int(flips.size),
-                flips=[dict(E_CO=float(eco[k]), E_O=float(eo[k]), device_status=int(st[k]),
-                            l10=float(l10[k]), l10_root=float(fx['l10_root'][k]), l10_tight=float(fx['l10_tight'][k]))
+    err = rel(l10, fx['l10_root'])            # l10_root: the oracle's answer (root, or the tight transient)
+    both_reg, both_deg = dev_reg & reg & ok, ~dev_reg & ~reg & ok
+    cov_reg = np.abs(y - fx['y_root']) <= RTOL * np.abs(fx['y_root']) + 1e-15
+    cov_deg = np.abs(y - fx['y_root']) <= RTOL * np.abs(fx['y_root']) + 1e-20
+    flips = np.nonzero((dev_reg != reg) & ok)[0]
+    uni = np.arange(n) < 2048                 # the uniform part of the fixture
+    info = dict(n=int(n), n_compared=int(ok.sum()), n_regular=int(dev_reg.sum()), n_not_reached=int((~dev_reg).sum()),
+                oracle_regular=int(reg.sum()), n_flips=int(flips.size),
+                flip_rate_uniform_nodes=float(np.mean((dev_reg != reg)[uni & ok])),
+                flips=[dict(E_CO=float(eco[k]), E_O=float(eo[k]), device_status=int(st[k]), l10=float(l10[k]),
+                            l10_oracle=float(fx['l10_root'][k]), l10_tight=float(fx['l10_tight'][k]),
+                            oracle_crit=float(fx['crit'][k]), oracle_newton_ok=bool(fx['newton_ok'][k]),
+                            max_rel_cov=float(np.max((np.abs(y[k] - fx['y_root'][k]) - 1e-20) /
+                                                     np.abs(fx['y_root'][k]))))
                        for k in flips],
-                max_rel_l10_regular=float(err_root.max()) if err_root.size else 0.0,
-                max_rel_l10_degenerate_vs_tight=float(err_tight.max()) if err_tight.size else 0.0,
-                max_abs_l10_degenerate_vs_tight=float(np.abs(l10[deg] - l10_t[deg]).max()) if deg.any() else 0.0,
-                reference_lsoda_vs_tight_max_abs_l10=float(np.abs(fx['l10_ref'] - fx['l10_tight'])[~reg].max()),
-                reference_lsoda_vs_tight_median_abs_l10=float(np.median(np.abs(fx['l10_ref'] - fx['l10_tight'])[~reg])),
-                least_squares_vs_device_max_abs_l10=float(np.abs(fx['l10_ls'][deg] - l10[deg]).max()) if deg.any() else 0.0,
-                least_squares_vs_device_max_abs_coverage=float(np.abs(fx['y_ls'][deg] - y[deg]).max()) if deg.any() else 0.0)
+                max_rel_l10_all=float(err[ok].max()),
+                max_rel_l10_regular=float(err[both_reg].max()) if both_reg.any() else 0.0,
+                max_rel_l10_not_reached=float(err[both_deg].max()) if both_deg.any() else 0.0,
+                reference_lsoda_vs_tight_max_abs_l10=float(np.nanmax(np.abs(fx['l10_ref'] - fx['l10_tight'])[ok])),
+                reference_lsoda_vs_device_max_abs_l10=float(np.nanmax(np.abs(fx['l10_ref'] - l10)[ok])))
+    ls_ok = np.isfinite(fx['l10_ls']) & ok
+    info['least_squares_within_1e-6_of_device'] = float(np.mean(rel(fx['l10_ls'][ls_ok], l10[ls_ok]) <= RTOL))
+    for key in ('l10_ref_reference', 'l10_ls_reference'):      # the reference's own code (make_volcano_reference.py)
+        if key in fx:
+            sel = np.isfinite(fx[key]) & ok
+            info[key + '_n'] = int(sel.sum())
+            info[key + '_within_1e-6_of_device'] = float(np.mean(rel(fx[key][sel], l10[sel]) <= RTOL))
+            info[key + '_max_abs_l10_vs_device'] = float(np.max(np.abs(fx[key][sel] - l10[sel])))
     _record('volcano_fixture_parity.json', info)
-    assert deg.sum() >= 256, info['n_degenerate']
-    assert np.all(err_root <= RTOL), (err_root.max(), np.nonzero(both)[0][np.argmax(err_root)])
-    assert np.all(cov_root)
-    assert np.all(err_tight <= RTOL), (err_tight.max(), np.nonzero(deg)[0][np.argmax(err_tight)])
-    bad = np.nonzero(~np.all(cov_tight, axis=1))[0]
-    assert bad.size == 0, [(int(np.nonzero(deg)[0][b]), y[deg][b].tolist(), y_t[deg][b].tolist()) for b in bad[:5]]
-    # boundary nodes.  Near the boundary of the two regimes the Newton
-    # iteration is chaotic (Jacobian condition up to 1e12): from the SAME start
-    # state the device and the oracle (LAPACK) can take different paths by
-    # rounding alone (tools/trace_newton.py, DESIGN.md "Steady state"), so the
-    # classification is allowed to differ on a few percent of this fixture --
-    # which over-samples that corner (512 of its 2 560 nodes) -- as long as
-    # every flipped node meets the bound of the semantics the device reports:
-    # status 4 -> the tight transient (checked above with the other status-4
-    # nodes); status 0 -> a root of the oracle's equations, every non-pivot
-    # species balanced to 1e-6 of its gross flux, non-negative.
-    uni = np.arange(n) < 2048                    # the uniform part of the fixture
-    info['flip_rate_uniform_nodes'] = float(np.mean((dev_reg != reg)[uni]))
-    _record('volcano_fixture_parity.json', info)
-    # measured: 73 of 2 560 (2.9 %), 1.5 % of the 2 048 uniform nodes (the
-    # grid-wide rate; binomial s.d. 0.3 %)
-    assert flips.size <= 0.05 * n, info['flips'][:10]
-    assert info['flip_rate_uniform_nodes'] <= 0.02, info['flip_rate_uniform_nodes']
-    spec = O.load_spec(os.path.join(inputs, 'COOxVolcano', 'input.json'))
-
-    def imbalance(k, yy):
-        """max |f_i| / gross_i over the non-pivot species of the oracle model at state yy"""
-        sp = copy.deepcopy(spec)
-        O.set_volcano_point(sp, eco[k], eo[k])
-        m = O.ClassicModel(sp)
-        full = m.y0.copy()
-        for q, nm in enumerate(names):
-            full[m.idx[nm]] = yy[q]
-        f, g = np.abs(m.rhs(full))[m.dyn], m.gross_flux(full)[m.dyn]
-        keep = np.ones(len(m.dyn), bool)
-        keep[list(O._rref(m.conservation())[1])] = False
-        return float(np.max(np.where(g[keep] > 0, f[keep] / np.where(g[keep] > 0, g[keep], 1.0), 0.0)))
-
-    # the reference's own steady-state algorithm (find_steady: least_squares
-    # from its lsoda transient, old_system.py:426-433) against the device's
-    # regular roots: equal to 1e-6 on log10 TOF at most nodes; where not, the
-    # device's state balances every species of the reference's equations (the
-    # record says how often least_squares' answer does not: stopped at xtol)
-    both_ok = both & fx['ok'] & np.isfinite(fx['l10_ls'])
-    ls_err = np.abs(fx['l10_ls'] - l10) / np.abs(l10)
-    agree = both_ok & (ls_err <= RTOL)
-    info['least_squares_agrees_on_regular'] = float(agree.sum() / max(both_ok.sum(), 1))
-    worse = []
-    for k in np.nonzero(both_ok & ~agree)[0][:40]:
-        worse.append((imbalance(k, fx['y_ls'][k]), imbalance(k, y[k])))
-    info['disagreeing_least_squares_vs_device_imbalance'] = worse
-    _record('volcano_fixture_parity.json', info)
-    assert info['least_squares_agrees_on_regular'] >= 0.85, info['least_squares_agrees_on_regular']
-    info['disagreeing_least_squares_also_a_root'] = int(sum(ref <= 1e-8 for ref, dev in worse))
-    _record('volcano_fixture_parity.json', info)
-    assert all(dev <= 1e-10 for ref, dev in worse), worse[:5]
-    for k in flips:
-        if st[k] == 0:
-            sp = copy.deepcopy(spec)
-            O.set_volcano_point(sp, eco[k], eo[k])
-            m = O.ClassicModel(sp)
-            full = m.y0.copy()
-            for q, nm in enumerate(names):
-                full[m.idx[nm]] = y[k, q]
-            assert np.all(full[m.dyn] >= 0.0), (eco[k], eo[k])
-            f = np.abs(m.rhs(full))[m.dyn]
-            g = m.gross_flux(full)[m.dyn]
-            keep = np.ones(len(m.dyn), bool)
-            keep[list(O._rref(m.conservation())[1])] = False
-            assert np.all(f[keep] <= 1e-6 * g[keep]), (eco[k], eo[k], (f / np.maximum(g, 1e-300))[keep])
+    if 'l10_ls_reference' in fx:
+        # the reference's own find_steady (least_squares from its lsoda
+        # transient) where the transient has reached the steady state: the
+        # device's root, at 1e-6 on all but a handful of nodes (measured
+        # 451 / 452 in the oracle: least_squares stops at xtol on the rest)
+        sel = ok & reg & dev_reg & np.isfinite(fx['l10_ls_reference'])
+        agree = rel(fx['l10_ls_reference'][sel], l10[sel]) <= RTOL
+        info['reference_find_steady_agrees_on_reached'] = [int(agree.sum()), int(sel.size and sel.sum())]
+        _record('volcano_fixture_parity.json', info)
+        assert agree.mean() >= 0.99, info['reference_find_steady_agrees_on_reached']
+        # the reference's own volcano driver value (lsoda at the input's rtol
+        # 1e-8 / atol 1e-10) is the device's answer up to that integrator's
+        # error: measured <= 1.04e-3 in log10(TOF) against the tight transient
+        sel = ok & fx['ref_ok_reference'] & np.isfinite(fx['l10_ref_reference'])
+        assert np.max(np.abs(fx['l10_ref_reference'][sel] - l10[sel])) <= 2e-3, info
+    assert np.all(err[ok] <= RTOL), (err[ok].max(), np.nonzero(ok)[0][np.argmax(err[ok])])
+    assert np.all(cov_reg[both_reg]), np.nonzero(both_reg & ~np.all(cov_reg, axis=1))[0][:5]
+    assert np.all(cov_deg[both_deg]), np.nonzero(both_deg & ~np.all(cov_deg, axis=1))[0][:5]
+    assert flips.size <= 0.01 * n, info['flips'][:10]
+    assert info['flip_rate_uniform_nodes'] <= 0.002, info['flip_rate_uniform_nodes']
+    for f in info['flips']:
+        assert 0.5 * ROOT_DIST <= f['oracle_crit'] <= 2.0 * ROOT_DIST, f
+        assert f['max_rel_cov'] <= 2.0 * ROOT_DIST + RTOL, f
 
 
 def test_degenerate_points_through_drop_in_api(P, inputs):

@@ -192,29 +192,35 @@ def test_volcano_drc(P, inputs, eps):
 
 
 def test_full_size_properties(P, inputs):
-    """1024 x 1024 volcano grid (BASELINE configs[2] per-GPU shard): every
-    solve converges, site balance holds, and sampled points match the oracle."""
+    """1024 x 1024 volcano grid (BASELINE configs[2] per-GPU shard) through
+    the drop-in volcano driver: every solve ends with a steady state reached
+    (status 0) or the transient end at t_end (4), the site balance holds, and
+    at sampled nodes (10 random, 4 of status 4) the activity equals the
+    oracle's answer by the same rule from its tight transient
+    (mk_oracle.steady_rule: lsoda at rtol 1e-11 / atol 1e-20) to 1e-6."""
     from pycatkin_amd.functions.volcano import volcano_activity
     s = P.read_from_input_file(os.path.join(inputs, 'COOxVolcano', 'input.json'))
     be = np.linspace(-2.5, 0.5, 1024)
     act, r = volcano_activity(s, be, be, steady=True)
     st = r['status']
     assert np.all((st == 0) | (st == 4))
-    assert np.mean(st == 4) < 0.15        # degenerate (O-poisoned) roots keep the transient end
+    assert np.mean(st == 4) < 0.15        # the O-poisoned corner, still moving at t_end
     assert np.all(np.isfinite(act))
     # site balance (the integrator rescales it after every step, Newton holds it)
     np.testing.assert_allclose(r['y'].sum(axis=0), 1.0, rtol=0, atol=1e-12)
     spec = O.load_spec(os.path.join(inputs, 'COOxVolcano', 'input.json'))
     rng = np.random.default_rng(11)
-    picks = list(rng.integers(0, be.size ** 2, 10)) + list(np.nonzero(st == 4)[0][:2])
+    picks = list(rng.integers(0, be.size ** 2, 10)) + list(rng.choice(np.nonzero(st == 4)[0], 4, replace=False))
+    done = 0
     for k in picks:
         i, j = divmod(int(k), be.size)
-        ref = O.volcano_point(spec, be[i], be[j], steady=bool(st[k] == 0))
-        if st[k] == 0:
-            assert ref['regular'], (be[i], be[j])
-        # status 4 keeps the transient end, integrated at the input's rtol 1e-8
-        tol = RTOL if st[k] == 0 else 1e-4
-        assert abs(act[i, j] - ref['activity']) <= tol * abs(ref['activity']), (be[i], be[j], st[k], act[i, j], ref['activity'])
+        ref = O.volcano_steady(spec, be[i], be[j])
+        if ref is None:                   # the oracle's integrators exceed their budget here
+            continue
+        done += 1
+        assert abs(act[i, j] - ref['activity']) <= RTOL * abs(ref['activity']), \
+            (be[i], be[j], st[k], ref['regular'], ref['crit'], act[i, j], ref['activity'])
+    assert done >= 10, done
 
 
 def test_edge_sizes(P, inputs):
@@ -401,39 +407,45 @@ def test_patch_order_matches_row_order(P, inputs):
     assert torch.equal(rt['status'].cpu(), torch.from_numpy(r['status']))
 
 
-def test_degenerate_roots_vs_least_squares(P, inputs):
-    """Status 4 (degenerate root, the O-poisoned corner): the device keeps the
-    transient state at t_end.  The reference's find_steady would run
-    least_squares(trf, xtol, ftol) from that state (old_system.py:426-429),
-    which stops wherever its tolerances let it on a root approached
-    algebraically: here it moves the free-site coverage from ~1e-5 towards 0.
-    Achieved bound (measured with the oracle's least_squares path): every
-    coverage within 2e-5 absolute of least_squares' answer; the activity
-    differs by up to 0.41 eV because log(TOF) follows the free-site coverage.
-    The device state itself is the reference's transient semantics
-    (System.activity, cooxvolcano.py:47) and matches it at 1e-4."""
+def test_not_reached_points_vs_reference_paths(P, inputs):
+    """Status 4 (the O-poisoned corner, whose transient is still moving at
+    t_end = 3600 s): the device reports the transient end, integrated at
+    STEADY_TRANSIENT -- the reference's System.activity semantics
+    (cooxvolcano.py:47) -- and it matches the oracle's tight transient
+    (lsoda, rtol 1e-11 / atol 1e-20) to 1e-6 on log10(TOF).  The reference's
+    own paths are recorded next to it, not asserted: its lsoda transient at
+    the input's rtol 1e-8 / atol 1e-10 (what cooxvolcano.py computes; its
+    tiny coverages sit under that atol) and the least_squares polish its
+    find_steady runs from there (old_system.py:385-433, with the reference's
+    transposed Jacobian), which stops wherever xtol lets it."""
+    import json
     from pycatkin_amd.functions.volcano import volcano_activity
     pts = [(-0.5, -2.5), (-0.5, -2.3), (0.0, -2.5), (0.0, -2.3), (0.0, -2.1)]
     s = P.read_from_input_file(os.path.join(inputs, 'COOxVolcano', 'input.json'))
     spec = O.load_spec(os.path.join(inputs, 'COOxVolcano', 'input.json'))
-    plan = None
     n4 = 0
+    rec = []
     for eco, eo in pts:
         act, r = volcano_activity(s, [eco], [eo], steady=True)
-        if r['status'][0] != 4:         # the corner's edge may classify as a (slow) regular root
-            assert r['status'][0] == 0
+        ref = O.volcano_steady(spec, eco, eo)
+        assert ref is not None
+        # activity = RT ln(h TOF / kB T): relative error ~ that of log(TOF)
+        assert abs(act[0, 0] - ref['activity']) <= RTOL * abs(ref['activity']), \
+            (eco, eo, int(r['status'][0]), act[0, 0], ref['activity'])
+        assert (r['status'][0] == 0) == ref['regular'] or 0.5e-6 <= ref['crit'] <= 2e-6, (eco, eo, ref['crit'])
+        if r['status'][0] != 4:
             continue
         n4 += 1
-        plan = plan or s.plan(('CO_ox',))
-        sp = copy.deepcopy(spec)
-        O.set_volcano_point(sp, eco, eo)
-        m = O.ClassicModel(sp)
-        yT, _ = m.solve_odes(rtol=1e-8, atol=1e-10)
-        yls = m.find_steady(yT.copy(), polish=False)
-        dyn = [m.idx[n] for n in plan.dyn]
-        assert np.max(np.abs(r['y'][:, 0] - yls[dyn])) <= 2e-5, (eco, eo, r['y'][:, 0], yls[dyn])
-        aT = m.activity(m.tof(yT, ['CO_ox']))
-        assert abs(act[0, 0] - aT) <= 1e-4 * abs(aT), (eco, eo, act[0, 0], aT)
+        m = ref['model']
+        yA, _ = m.solve_odes(rtol=1e-8, atol=1e-10, method='LSODA')
+        yls = m.find_steady(yA.copy(), polish=False)
+        rec.append(dict(E_CO=eco, E_O=eo, device_activity=float(act[0, 0]), oracle_activity=float(ref['activity']),
+                        oracle_tight_l10=float(np.log10(ref['tof'])),
+                        reference_lsoda_l10=float(np.log10(m.tof(yA, ['CO_ox']))),
+                        least_squares_l10=float(np.log10(max(m.tof(yls, ['CO_ox']), 1e-300))),
+                        least_squares_status=int(m.ls_status)))
+    if os.path.isdir('gpurun_out'):
+        json.dump(rec, open('gpurun_out/not_reached_vs_reference_paths.json', 'w'), indent=1)
     assert n4 >= 3, n4
 
 
@@ -574,7 +586,7 @@ def test_wave_order_does_not_change_results(P, inputs):
     4 lanes per wavefront, then the wavefronts longest-first) only changes
     WHEN each 64-condition wavefront runs, not which conditions share it:
     every output is bitwise equal to the launch-order solve (512 x 512 grid in
-    16 x 4 patch order, Newton and the degenerate-root retry included)."""
+    16 x 4 patch order, the bench's steady-state rule)."""
     import torch
     from pycatkin_amd.functions.volcano import set_volcano_energies, tile_order
     from pycatkin_amd import _lib as L
@@ -592,7 +604,7 @@ def test_wave_order_does_not_change_results(P, inputs):
     T, p, d, fx, y0, inflow = s._inputs(net, plan, n, np.full(n, 600.0), None,
                                         {'ECO': E1.ravel()[perm], 'EO': E2.ravel()[perm]}, None, None, None)
     cond, keep = net.conditions(n, T, p, d, fx, y0, inflow)
-    from pycatkin_amd.classes.system import DEGENERATE_RETRY
+    from pycatkin_amd.classes.system import ROOT_DIST, STEADY_TRANSIENT
     res = {}
     for mode in (-1, 1):
         out = dict(y=torch.empty((net.NDYN, n), dtype=torch.float64, device='cuda'),
@@ -602,8 +614,8 @@ def test_wave_order_does_not_change_results(P, inputs):
         o = L.Outputs()
         o.y, o.ld_y, o.tof, o.status, o.nsteps = _ptr(out['y']), n, _ptr(out['tof']), _ptr(out['status']), \
             _ptr(out['nsteps'])
-        prm = net.params(t0=0.0, t_end=3600.0, rtol=1e-8, atol=1e-10, max_steps=200000, newton=True,
-                         retry=DEGENERATE_RETRY, wave_order=mode)
+        prm = net.params(t0=0.0, t_end=3600.0, rtol=STEADY_TRANSIENT[0], atol=STEADY_TRANSIENT[1],
+                         max_steps=200000, newton=True, root_dist=ROOT_DIST, wave_order=mode)
         L.check(net.lib.pck_solve(net.h, C.byref(cond), C.byref(prm), C.byref(o),
                                   C.c_void_p(torch.cuda.current_stream().cuda_stream)))
         res[mode] = {k: v.cpu().numpy() for k, v in out.items()}

@@ -197,3 +197,67 @@ def test_species_jacobian_is_exact(inputs, net):
         ym[q] -= hq
         fd = (m.species_odes(yp) - m.species_odes(ym)) / (2.0 * hq)
         np.testing.assert_allclose(J[:, q], fd, rtol=1e-6, atol=1e-6 * (np.abs(J).max() + 1e-300))
+
+
+def test_vectorised_model_matches_line_by_line_restatement(inputs):
+    """ClassicModel's array forms of rates / species_odes / species_jacobian
+    equal the line-by-line restatements of old_system.py:202-313
+    (rates_loop, species_odes_loop, species_jacobian_loop) to rounding, with
+    and without a DRC perturbation, on every network the tests use."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__)))
+    from _synth import spec_of
+    from pycatkin_amd.functions.synthetic import synthetic_network
+    rng = np.random.default_rng(4)
+    vol = O.load_spec(os.path.join(inputs, 'COOxVolcano', 'input.json'))
+    O.set_volcano_point(vol, -1.0, -1.2)
+    specs = [O.load_spec(os.path.join(inputs, 'DMTM', 'input.json')), vol,
+             O.load_spec(os.path.join(inputs, 'COOxReactor', 'input_Pd111.json')),
+             spec_of(synthetic_network(), rng.uniform(-0.5, 0.5, 4))]
+    for spec in specs:
+        m = O.ClassicModel(spec)
+        for t in range(3):
+            y = rng.uniform(0.0, 1.0, len(m.snames))
+            y[rng.integers(len(y))] = 0.0 if t == 2 else y[0]
+            m.perturb[:] = 0.0
+            if t == 1:
+                m.perturb[0] = 1e-3 * m.kf[0]
+            np.testing.assert_allclose(m.rates(y), m.rates_loop(y), rtol=1e-14, atol=0.0)
+            fb = m.species_odes_loop(y)
+            np.testing.assert_allclose(m.species_odes(y), fb, rtol=0.0, atol=1e-14 * np.abs(fb).max())
+            Jb = m.species_jacobian_loop(y)
+            np.testing.assert_allclose(m.species_jacobian(y), Jb, rtol=0.0, atol=1e-14 * np.abs(Jb).max())
+
+
+def test_volcano_fixture_pinned_by_reference_run():
+    """tests/golden/volcano_fixture.npz: the oracle's restated reference
+    columns against the reference's own code run on 768 of its nodes
+    (make_volcano_reference.py: old_system.solve_odes with lsoda at the
+    input's tolerances and nsteps, then old_system.find_steady):
+      * lsoda transient: the restatement integrates without the 1e5 output
+        stops, so the two differ by lsoda's error at the input tolerances --
+        median 1.5e-9, at most 1.05e-3 in log10(TOF) (the poisoned corner);
+      * where the transient has reached a steady state (`regular`), the
+        reference's least_squares answer is the oracle's root to 1e-6 on
+        >= 99 % of the nodes (xtol stops it short on the rest)."""
+    fx = dict(np.load(os.path.join(HERE, 'golden', 'volcano_fixture.npz')))
+    if 'l10_ref_reference' not in fx:
+        pytest.skip('fixture without the reference columns (run make_volcano_reference.py)')
+    sel = fx['ref_done_reference'] & fx['ref_ok_reference'] & np.isfinite(fx['l10_ref'])
+    assert sel.sum() >= 760
+    d = np.abs(fx['l10_ref_reference'][sel] - fx['l10_ref'][sel])
+    assert np.median(d) <= 1e-8 and d.max() <= 2e-3, (np.median(d), d.max())
+    reg = sel & fx['regular'] & fx['tight_ok'] & np.isfinite(fx['l10_ls_reference'])
+    agree = np.abs(fx['l10_ls_reference'][reg] - fx['l10_root'][reg]) <= 1e-6 * np.abs(fx['l10_root'][reg])
+    assert reg.sum() >= 400 and agree.mean() >= 0.99, (reg.sum(), agree.mean())
+
+
+def test_fixture_rule_constants_match_the_product():
+    """The fixtures restate the device's steady-state rule with the product's
+    ROOT_DIST and STEADY_TRANSIENT atol."""
+    from pycatkin_amd.classes.system import ROOT_DIST, STEADY_TRANSIENT
+    fx = np.load(os.path.join(HERE, 'golden', 'volcano_fixture.npz'))
+    assert tuple(fx['root_dist']) == (ROOT_DIST, STEADY_TRANSIENT[1])
+    path = os.path.join(HERE, 'golden', 'synthetic_fixture.npz')
+    if os.path.isfile(path):
+        assert tuple(np.load(path)['root_dist']) == (ROOT_DIST, STEADY_TRANSIENT[1])
