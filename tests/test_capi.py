@@ -82,9 +82,14 @@ def _kernel_metadata(lib_path, tmp_path):
     """name -> (vgpr_count, agpr_count, private_segment_fixed_size) of every
     kernel in the library's gfx950 code object (read with the ROCm LLVM tools,
     no GPU)."""
+    import shutil
     import subprocess
     fb, elf = str(tmp_path / 'fb.bin'), str(tmp_path / 'k.elf')
-    subprocess.run(['objcopy', '--dump-section', '.hip_fatbin=' + fb, lib_path], check=True)
+    # objcopy with no output file rewrites its input in place: work on a copy,
+    # never on the library this process (or a later GPU run) has mapped
+    cp = str(tmp_path / 'lib_copy.so')
+    shutil.copyfile(lib_path, cp)
+    subprocess.run(['objcopy', '--dump-section', '.hip_fatbin=' + fb, cp], check=True)
     subprocess.run([LLVM + '/clang-offload-bundler', '--type=o', '--input=' + fb,
                     '--targets=hipv4-amdgcn-amd-amdhsa--gfx950', '--output=' + elf, '--unbundle'], check=True)
     notes = subprocess.run([LLVM + '/llvm-readelf', '--notes', elf], check=True, capture_output=True,
