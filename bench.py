@@ -13,17 +13,16 @@ ranks come from the environment.  The conditions are independent, so ranks
 share nothing in the timed region; one RCCL all_gather of the results follows
 it.
 
-  --scaling weak (default)    every rank solves its own 1024 x 1024 share of an
-                              (N*1024) x 1024 grid: rank r solves E_CO rows
-                              r, r+N, ... (every rank samples the whole volcano);
-                              the per-GPU work is BASELINE configs[2]'s grid at
-                              every N (the task's rule for a path that
-                              partitions into independent units)
-  --scaling strong            the fixed 1024 x 1024 grid sharded over the N
-                              ranks (cyclic rows as above): at N = 8 each GPU
-                              holds 2 048 wavefronts for 3 072 wave slots and
-                              runs at the latency of its slowest wavefronts
-                              (DESIGN.md "Multi-GPU"; tools/emulate_scaling.py)
+  --scaling strong (default)  BASELINE configs[2]: the fixed 1024 x 1024 grid
+                              sharded over the N ranks, rank r solving E_CO
+                              rows r, r+N, ... (cyclic rows: every rank samples
+                              the whole volcano).  At N = 8 each GPU holds
+                              2 048 wavefronts for 3 072 wave slots and runs at
+                              the latency of its slowest wavefronts (DESIGN.md
+                              "Multi-GPU"; tools/emulate_scaling.py)
+  --scaling weak              every rank solves its own 1024 x 1024 share of an
+                              (N*1024) x 1024 grid (the same cyclic rows):
+                              the per-GPU work stays BASELINE's grid at every N
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--scaling strong|weak]
                     [--config volcano|cstr|dmtm_drc|ch4|synthetic]
@@ -167,6 +166,18 @@ def host_cores():
 # nproc / os.cpu_count() report the whole machine there); the CPU baseline runs
 # one worker per CPU of that share.
 BOX_CPU_SHARE = 16
+
+
+# which reference path the CPU baseline's oracle call restates, per config
+CPU_PATH = dict(
+    volcano='System.solve_odes with ode_solver "ode" (lsoda, the input\'s rtol 1e-8 / atol 1e-10) then the Newton '
+            'polish of find_steady (old_system.py:315-468), i.e. activity(ss_solve=True) after a transient; the '
+            'reference\'s own activity() runs at 0.79x this port per core (profiles/r3/cpu_reference_vs_port.json)',
+    cstr='System.solve_odes (lsoda) + find_steady on the Pd111 CSTR (presets.run_temperatures, '
+         'steady_state_solve=True)',
+    dmtm_drc='System.degree_of_rate_control (2R+1 transients, old_system.py:490-515)',
+    ch4='SteadyStateSolver.solve_ode (scipy BDF to 1e4 s, solver.py:374-418)',
+    synthetic='System.solve_odes (scipy BDF) + find_steady on the synthetic network')
 
 
 def _cpu_warm(_):
@@ -535,7 +546,7 @@ def build_parser():
     ap.add_argument('--steps', type=int, default=10)
     ap.add_argument('--warmup', type=int, default=2)
     ap.add_argument('--config', choices=sorted(CONFIGS), default='volcano')
-    ap.add_argument('--scaling', choices=('strong', 'weak'), default='weak')
+    ap.add_argument('--scaling', choices=('strong', 'weak'), default='strong')
     ap.add_argument('--grid', type=int, default=1024)
     ap.add_argument('--n', type=int, default=0, help='conditions of the non-volcano configs (0: config default)')
     ap.add_argument('--max-steps', type=int, default=200000, help='integrator step budget per condition (library default)')
@@ -707,17 +718,21 @@ def main(argv=None):
                     '64 x (ADD+MUL+TRANS) + 128 x FMA fp64 wave instructions of the committed PMC profile of this '
                     'workload, per launch x solver launches per step)',
                     'integrator_steps': steps_local, 'lane_efficiency': lane_eff, 'solver_launches_per_step': nl}
-            if world == 1 and not args.no_cpu_baseline:
+            if not args.no_cpu_baseline:
+                # N > 1: stated once for the node, on rank 0 after the timed
+                # region (the other ranks wait in the closing barrier); the
+                # node's CPU share is BOX_CPU_SHARE per GPU
                 avail = host_cores()
-                workers = min(BOX_CPU_SHARE, avail)
+                workers = min(BOX_CPU_SHARE * world, avail)
                 log('cpu baseline: %d points, %d workers' % (args.cpu_points, workers))
                 v, dt, done = cpu_baseline(args.config, args.cpu_points, workers)
                 cpu_line = dict(value=v, unit='%s/s' % wl.units, cores=workers, kind='port',
                                 sample='%d random units of the same %s workload solved in %.1f s by the oracle '
-                                       '(numpy/scipy restatement of the reference path), %d single-threaded worker '
-                                       'processes = the one-GPU box\'s CPU share (affinity/cgroup show %d, '
-                                       'os.cpu_count() %d for the whole host)'
-                                       % (done, args.config, dt, workers, avail, os.cpu_count() or 0))
+                                       '(numpy/scipy restatement of the reference path: %s), %d single-threaded '
+                                       'worker processes = %d GPU(s) x the %d-CPU share per GPU (affinity/cgroup '
+                                       'show %d, os.cpu_count() %d for the whole host)'
+                                       % (done, args.config, dt, CPU_PATH.get(args.config, ''), workers, world,
+                                          BOX_CPU_SHARE, avail, os.cpu_count() or 0))
         line = {
             'metric': METRIC if args.config == 'volcano' else
             '%s/sec (whole node), BASELINE config %s' % (wl.units, args.config),

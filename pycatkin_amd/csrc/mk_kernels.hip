@@ -1015,6 +1015,11 @@ static int launch_solve(const pck_network* net, const pck_conditions* cond, cons
         SolveArgs pv = a;
         pv.rtol = fmax(a.rtol, 1e-3);
         pv.atol = a.atol * (pv.rtol / a.rtol);       // the same atol / rtol ratio
+        {
+            // A/B: PCK_PREVIEW_ATOL = a floor of the preview's atol, relative to its rtol
+            const char* e = getenv("PCK_PREVIEW_ATOL");
+            if (e) pv.atol = fmax(pv.atol, atof(e) * pv.rtol);
+        }
         pv.newton = 0;
         pv.max_steps = a.max_steps < 1000 ? a.max_steps : 1000;
         pv.y = nullptr; pv.tof = nullptr; pv.status = nullptr; pv.nsteps = pns;

@@ -15,7 +15,8 @@ mk_oracle.steady_rule -- the device's steady-state rule
   root     Newton from `tight`; the answer (`regular`) only where `tight`
            lies within ROOT_DIST * |root| + STEADY_ATOL of it, else `tight`
            itself; `newton_ok` / `crit` as in make_volcano_fixture.py
-  l10      log10 of the answer's TOF (reaction R0, the bench's tof_terms)
+  tof, l10 the answer's TOF (net rate of reaction R0, the bench's tof_terms;
+           negative where G0 desorbs on balance) and its log10 (-inf there)
 
     OMP_NUM_THREADS=1 python tests/golden/make_synthetic_fixture.py [--workers 8]
 
@@ -65,14 +66,14 @@ def _cond(arg):
     nan = np.full(len(dyn), np.nan)
     if r is None:
         return k, dict(ok=False, regular=False, newton_ok=False, crit=np.inf, y_tight=nan, y_root=nan,
-                       l10=np.nan, l10_tight=np.nan, seconds=time.time() - t), [m.snames[i] for i in dyn]
+                       l10=np.nan, l10_tight=np.nan, tof=np.nan, seconds=time.time() - t), [m.snames[i] for i in dyn]
 
     def l10(y):
         v = m.tof(y, ['R0'])
         return np.log10(v) if v > 0 else -np.inf
     return k, dict(ok=True, regular=r['regular'], newton_ok=r['newton_ok'], crit=r['crit'],
                    y_tight=r['y_tight'][dyn], y_root=r['y'][dyn], l10=l10(r['y']), l10_tight=l10(r['y_tight']),
-                   seconds=time.time() - t), [m.snames[i] for i in dyn]
+                   tof=m.tof(r['y'], ['R0']), seconds=time.time() - t), [m.snames[i] for i in dyn]
 
 
 def main():
@@ -94,7 +95,7 @@ def main():
     arr = dict(idx=np.array(idx, np.int64), desc=D[idx], dyn=np.array(names), root_dist=np.array([ROOT_DIST, STEADY_ATOL]))
     for f in ('ok', 'regular', 'newton_ok'):
         arr[f] = np.array([res[k][f] for k in idx], bool)
-    for f in ('crit', 'l10', 'l10_tight', 'seconds'):
+    for f in ('crit', 'l10', 'l10_tight', 'tof', 'seconds'):
         arr[f] = np.array([res[k][f] for k in idx], float)
     for f in ('y_tight', 'y_root'):
         arr[f] = np.array([res[k][f] for k in idx], float)

@@ -41,12 +41,12 @@ def test_launcher_world2(scaling, grid):
     assert line['value'] > 0
 
 
-def test_default_multi_gpu_layout_is_weak():
-    """Without --scaling, N ranks each solve a full G x G share: the per-GPU
-    work is BASELINE configs[2]'s grid at every N."""
+def test_default_multi_gpu_layout_is_strong():
+    """Without --scaling, the N ranks shard one fixed G x G grid: BASELINE
+    configs[2]'s 1024 x 1024 grid sharded over the GPUs of the node."""
     line = _run(['--gpus', '2', '--steps', '1', '--warmup', '0', '--grid', '16'])
-    assert line['scaling'] == 'weak'
-    assert line['config']['global_grid'] == [32, 16] and line['config']['grid_per_gpu'] == [16, 16]
+    assert line['scaling'] == 'strong'
+    assert line['config']['global_grid'] == [16, 16] and line['config']['grid_per_gpu'] == [8, 16]
 
 
 def test_launcher_single_rank():

@@ -23,8 +23,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def shard_ms(bench, torch, scaling, rank, world, steps):
-    args = bench.build_parser().parse_args(['--scaling', scaling])
+def shard_ms(bench, torch, scaling, rank, world, steps, extra=()):
+    args = bench.build_parser().parse_args(['--scaling', scaling] + list(extra))
     wl = bench.volcano_workload(args, rank, world)
     sp = C.c_void_p(torch.cuda.current_stream().cuda_stream)
     for _ in range(3):                 # warm-up: clocks and the pool allocator settle
@@ -47,20 +47,25 @@ def shard_ms(bench, torch, scaling, rank, world, steps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--steps', type=int, default=3)
+    ap.add_argument('--worlds', default='1,2,4,8', help='strong-scaling world sizes')
+    ap.add_argument('--no-weak', action='store_true')
+    ap.add_argument('--bench-args', default='', help="extra bench.py arguments, ','-separated (A/B)")
     a = ap.parse_args()
+    extra = [x for x in a.bench_args.split(',') if x]
     import torch
     import bench
     out = []
-    for scaling, worlds in (('strong', (1, 2, 4, 8)), ('weak', (8,))):
+    plan = [('strong', tuple(int(w) for w in a.worlds.split(',')))] + ([] if a.no_weak else [('weak', (8,))])
+    for scaling, worlds in plan:
         for N in worlds:
-            ranks = [shard_ms(bench, torch, scaling, r, N, a.steps) for r in range(N)]
+            ranks = [shard_ms(bench, torch, scaling, r, N, a.steps, extra) for r in range(N)]
             t = max(x['ms'] for x in ranks)
             units = sum(x['units'] for x in ranks)
-            line = dict(scaling=scaling, n_gpus=N, rank_ms=[x['ms'] for x in ranks], max_rank_ms=t,
+            line = dict(scaling=scaling, n_gpus=N, bench_args=extra, rank_ms=[x['ms'] for x in ranks], max_rank_ms=t,
                         predicted_value=units / (t * 1e-3), units=units, ranks=ranks)
             print(json.dumps(line), flush=True)
             out.append(line)
-    base = [x for x in out if x['scaling'] == 'strong' and x['n_gpus'] == 1][0]['predicted_value']
+    base = [x for x in out if x['scaling'] == 'strong'][0]['predicted_value']
     for x in out:
         x['predicted_speedup_vs_1'] = x['predicted_value'] / base
     print(json.dumps(dict(summary=[{k: x[k] for k in ('scaling', 'n_gpus', 'max_rank_ms', 'predicted_value',
