@@ -199,10 +199,12 @@ const char* pck_last_error(void);
 int pck_network_create(const int32_t* ip, int64_t n_ip, const double* dp, int64_t n_dp,
                        pck_network** out);
 int pck_network_destroy(pck_network* net);
-/* Sizes of a created network: dims[0..9] = D, NTH, NREG, NRXN, NDYN, NFIX, NCONS, NTOF,
+/* Sizes of a created network: dims[0..10] = D, NTH, NREG, NRXN, NDYN, NFIX, NCONS, NTOF,
  * n_features, plan id: a compiled-in plan (csrc/networks.h), PCK_PLAN_ID_JIT once a
  * lane solve ran the plan hipRTC specialised for this network (csrc/mk_jit.h;
- * PCK_JIT=0 in the environment disables it), 0 = runtime plan. */
+ * PCK_JIT=0 in the environment disables it), 0 = runtime plan; and the kernel of the
+ * last lane-group solve: 0 compiled-in record tables, 1 hipRTC exact-size record
+ * tables, 2 hipRTC with the network compiled in (PCK_GRP_CT=0 disables it). */
 #define PCK_PLAN_ID_JIT 100
 int pck_network_dims(const pck_network* net, int32_t* dims);
 /* Solver selection (A/B checks): PCK_PLAN_AUTO (default: compiled-in plan when

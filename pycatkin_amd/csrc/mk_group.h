@@ -374,9 +374,165 @@ __device__ __forceinline__ void put_c(const Grp<NSP>& x, double y) {
     wsync();
 }
 
+// ---------------------------------------------------------------------------
+// Compile-time network (the hipRTC build of csrc/mk_jit.h: jit_group_ct_kernel).
+// With the network's tables constexpr (nets::Jit: exponents, stoichiometry,
+// concentration factors), every lane of a group evaluates every reaction of
+// its condition in straight-line code: the group's concentrations are
+// broadcast into registers (DPP row_newbcast on 16-lane groups, v_readlane on
+// a wavefront), the rates and their derivatives are products with compile-time
+// exponents, and each lane keeps its own species row -- the row sums with
+// compile-time coefficients.  No record decode, no CSR walk, no LDS traffic
+// but the condition's k_eff (one broadcast read per reaction), no barrier.
+// The record-table path (above: lane-per-reaction, then the CSR gather) does
+// the same arithmetic in another order: the two agree to rounding.
+// ---------------------------------------------------------------------------
+struct NoNet {};
+template <class Net> struct IsCt { static constexpr bool v = true; };
+template <> struct IsCt<NoNet> { static constexpr bool v = false; };
+
+// lane q of the calling lane's group, q a compile-time constant after unrolling
+template <int G>
+__device__ __forceinline__ double gbcast_k(double v, int q) {
+    if constexpr (G == 16) {
+        return bc16(v, q);
+    } else if constexpr (G == 64) {
+        return rlane(v, q);
+    } else {
+        const double a = rlane(v, q), b = rlane(v, 32 + q);
+        return (threadIdx.x & 32) ? b : a;
+    }
+}
+
+// row sums by per-row accumulators (cheaper for small networks) or by the
+// lane's coefficient of each column (fewer registers)
+#ifndef PCK_CT_ACC_MAX
+#define PCK_CT_ACC_MAX 24
+#endif
+
+template <class Net, int NSP, int G, bool CL>
+__device__ __forceinline__ void ct_conc(const Grp<NSP>& x, double y, double (&c)[Net::NS]) {
+    const double v = (CL && PCK_GRP_CLAMP) ? fmax(y, 0.0) : y;
+#pragma unroll
+    for (int q = 0; q < Net::NS; ++q) c[q] = Net::dyn(q, 0) * gbcast_k<G>(v, q);
+}
+
+// S(gl, j): the calling lane's coefficient of column j (0 off its row)
+template <class Net, int NSP>
+__device__ __forceinline__ double ct_coef(const Grp<NSP>& x, int j) {
+    double s = 0.0;
+#pragma unroll
+    for (int i = 0; i < Net::NS; ++i)
+        if (Net::S(i, j) != 0.0) s = (x.gl == i) ? Net::S(i, j) : s;
+    return s;
+}
+
+template <class Net>
+__device__ __forceinline__ bool ct_col_used(int j) {
+    bool u = false;
+#pragma unroll
+    for (int i = 0; i < Net::NS; ++i) u = u || (Net::S(i, j) != 0.0);
+    return u;
+}
+
+// forward / reverse rate of reaction j (kf, kr: the condition's effective constants)
+template <class Net>
+__device__ __forceinline__ void ct_rate(int j, double kf, double kr, const double (&c)[Net::NS], double& rf,
+                                        double& rr) {
+    rf = kf;
+    rr = kr;
+#pragma unroll
+    for (int i = 0; i < Net::NS; ++i) {
+        if (Net::ef(j, i)) rf *= ipow(c[i], Net::ef(j, i));
+        if (Net::er(j, i)) rr *= ipow(c[i], Net::er(j, i));
+    }
+}
+
+// f (and with GROSS the gross flux g) of the calling lane's row
+template <class Net, int NSP, int G, bool CL, bool GROSS = false>
+__device__ __forceinline__ double ct_rhs(const Grp<NSP>& x, double y, double* gross = nullptr) {
+    constexpr int NS = Net::NS, R = Net::R;
+    double c[NS];
+    ct_conc<Net, NSP, G, CL>(x, y, c);
+    double f = 0.0, gacc = 0.0;
+    if constexpr (NS <= PCK_CT_ACC_MAX && !GROSS) {
+        double acc[NS];
+#pragma unroll
+        for (int i = 0; i < NS; ++i) acc[i] = 0.0;
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            if (!ct_col_used<Net>(j)) continue;
+            double rf, rr;
+            ct_rate<Net>(j, x.kf[j], x.kr[j], c, rf, rr);
+            const double net = rf - rr;
+#pragma unroll
+            for (int i = 0; i < NS; ++i)
+                if (Net::S(i, j) != 0.0) acc[i] += Net::S(i, j) * net;
+        }
+#pragma unroll
+        for (int i = 0; i < NS; ++i) f = (x.gl == i) ? acc[i] : f;
+    } else {
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            if (!ct_col_used<Net>(j)) continue;
+            double rf, rr;
+            ct_rate<Net>(j, x.kf[j], x.kr[j], c, rf, rr);
+            const double s = ct_coef<Net>(x, j);
+            f = fma(s, rf - rr, f);
+            if constexpr (GROSS) gacc = fma(fabs(s), fabs(rf) + fabs(rr), gacc);
+        }
+    }
+    if (!x.row) return 0.0;
+    if constexpr (GROSS) *gross = gacc * fabs(x.rs) + fabs(x.fl) * (fabs(x.in) + fabs(y));
+    return f * x.rs + x.fl * (x.in - y);
+}
+
+// W[q] = sgn * dF_i/dy_q + (q == i ? shift : 0) on the calling lane's row i
+template <class Net, int NSP, int G, bool CL>
+__device__ __forceinline__ void ct_jac(const Grp<NSP>& x, double y, double sgn, double shift, double (&W)[NSP]) {
+    constexpr int NS = Net::NS, R = Net::R;
+    double c[NS];
+    ct_conc<Net, NSP, G, CL>(x, y, c);
+    double jr[NS];
+#pragma unroll
+    for (int q = 0; q < NS; ++q) jr[q] = 0.0;
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+        if (!ct_col_used<Net>(j)) continue;
+        const double s = ct_coef<Net>(x, j);
+        const double kf = x.kf[j], kr = x.kr[j];
+        // d net_j / d y_q for every participant q (mk_solver.h: jac)
+#pragma unroll
+        for (int q = 0; q < NS; ++q) {
+            if (!(Net::ef(j, q) || Net::er(j, q))) continue;
+            double v = 0.0;
+            if (Net::ef(j, q)) {
+                double t = kf * (double)Net::ef(j, q) * Net::dyn(q, 0) * ipow(c[q], Net::ef(j, q) - 1);
+#pragma unroll
+                for (int i = 0; i < NS; ++i)
+                    if (i != q && Net::ef(j, i)) t *= ipow(c[i], Net::ef(j, i));
+                v += t;
+            }
+            if (Net::er(j, q)) {
+                double t = kr * (double)Net::er(j, q) * Net::dyn(q, 0) * ipow(c[q], Net::er(j, q) - 1);
+#pragma unroll
+                for (int i = 0; i < NS; ++i)
+                    if (i != q && Net::er(j, i)) t *= ipow(c[i], Net::er(j, i));
+                v -= t;
+            }
+            jr[q] = fma(s, v, jr[q]);
+        }
+    }
+    const double sc = sgn * x.rs;
+    const double dg = shift - sgn * x.fl;
+#pragma unroll
+    for (int q = 0; q < NSP; ++q) W[q] = (x.row && q < NS) ? sc * jr[q < NS ? q : 0] + (q == x.gl ? dg : 0.0) : 0.0;
+}
+
 // f_i = rs_i * sum_r S_ir net_r + fl_i (in_i - y_i)   (row lanes; 0 elsewhere)
-template <int NSP, int G, bool CL = false>
+template <int NSP, int G, bool CL = false, class Net = NoNet>
 __device__ __forceinline__ double grp_rhs(const GrpView& g, const Grp<NSP>& x, double y) {
+    if constexpr (IsCt<Net>::v) return ct_rhs<Net, NSP, G, CL>(x, y);
     put_c<NSP, CL>(x, y);
     for (int r = x.gl; r < x.R; r += G) x.d[r] = rec_rate(g.rx[r], x.kf[r], x.kr[r], x.c);
     wsync();
@@ -447,9 +603,13 @@ __device__ __forceinline__ double grp_rhs(const GrpView& g, const Grp<NSP>& x, d
 
 // W[q] = sgn * dF_i/dy_q + (q == i ? shift : 0), with dF/dy including the flow
 // diagonal (-fl_i); 0 on lanes without a row
-template <int NSP, int G, int P, bool CL = false>
+template <int NSP, int G, int P, bool CL = false, class Net = NoNet>
 __device__ __forceinline__ void grp_jac(const NetView& nv, const GrpView& g, const Grp<NSP>& x, double y, double sgn,
                                         double shift, double (&W)[NSP]) {
+    if constexpr (IsCt<Net>::v) {
+        ct_jac<Net, NSP, G, CL>(x, y, sgn, shift, W);
+        return;
+    }
     constexpr int QB = (NSP + P - 1) / P;
     put_c<NSP, CL>(x, y);
     for (int r = x.gl; r < x.R; r += G) {
@@ -747,7 +907,7 @@ __device__ __forceinline__ double grp_solve(const Grp<NSP>& x, const LU<NSP>& F,
 // RODAS4 on the group (same scheme, controller, projection and positivity
 // rule as mk_solver.h: integrate)
 // ---------------------------------------------------------------------------
-template <int NSP, int G, int P, bool TRAJ = false>
+template <int NSP, int G, int P, bool TRAJ = false, class Net = NoNet>
 __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& gv, const Grp<NSP>& x, double& y,
                                              double t0, double t_end, double rtol, double atol, int max_steps,
                                              int& nsteps, bool crows, const TrajOut& to, LU<NSP>& F) {
@@ -769,7 +929,7 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
         }
         return PCK_ST_OK;
     }
-    double F0 = grp_rhs<NSP, G, CLAMP>(gv, x, y);
+    double F0 = grp_rhs<NSP, G, CLAMP, Net>(gv, x, y);
     double cons0[PCK_MAX_CONS];
     double ci[PCK_MAX_CONS];
     bool cpos[PCK_MAX_CONS];
@@ -788,7 +948,7 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
         const double d1 = sqrt(gsum<G>(x.row ? (F0 / sc) * (F0 / sc) : 0.0) * invNS);
         double h0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : 0.01 * d0 / d1;
         h0 = fmin(h0, span);
-        const double F1 = grp_rhs<NSP, G, CLAMP>(gv, x, y + h0 * F0);
+        const double F1 = grp_rhs<NSP, G, CLAMP, Net>(gv, x, y + h0 * F0);
         const double q = (F1 - F0) / sc;
         const double d2 = sqrt(gsum<G>(x.row ? q * q : 0.0) * invNS) / h0;
         const double h1 = (d1 <= 1e-15 && d2 <= 1e-15) ? fmax(1e-6, h0 * 1e-3) : pow(0.01 / fmax(d1, d2), 0.2);
@@ -812,7 +972,7 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
         const bool tr = (x.cidx == pck_trace_cond) && x.gl == 0;
         if (tr) pck_phase[5] += 1.0;
 #endif
-        PCK_PH(0, (grp_jac<NSP, G, P, CLAMP>(nv, gv, x, y, -1.0, ig, F.W)));       // W = I/(h g) - J
+        PCK_PH(0, (grp_jac<NSP, G, P, CLAMP, Net>(nv, gv, x, y, -1.0, ig, F.W)));       // W = I/(h g) - J
         if (cpv >= 0) {                                        // conservation rows (mk_solver.h: cons_rows)
             double m = 0.0;
 #pragma unroll
@@ -843,14 +1003,14 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
         }
         double k1, k2, k3, k4, k5, k6, fu, u;
         PCK_PH(2, (k1 = grp_solve<NSP, G>(x, F, keep * F0)));
-        PCK_PH(3, (fu = grp_rhs<NSP, G, CLAMP>(gv, x, y + a21 * k1)));
+        PCK_PH(3, (fu = grp_rhs<NSP, G, CLAMP, Net>(gv, x, y + a21 * k1)));
         PCK_PH(2, (k2 = grp_solve<NSP, G>(x, F, keep * (fu + ih * (C21 * k1)))));
-        PCK_PH(3, (fu = grp_rhs<NSP, G, CLAMP>(gv, x, y + a31 * k1 + a32 * k2)));
+        PCK_PH(3, (fu = grp_rhs<NSP, G, CLAMP, Net>(gv, x, y + a31 * k1 + a32 * k2)));
         PCK_PH(2, (k3 = grp_solve<NSP, G>(x, F, keep * (fu + ih * (C31 * k1 + C32 * k2)))));
-        PCK_PH(3, (fu = grp_rhs<NSP, G, CLAMP>(gv, x, y + a41 * k1 + a42 * k2 + a43 * k3)));
+        PCK_PH(3, (fu = grp_rhs<NSP, G, CLAMP, Net>(gv, x, y + a41 * k1 + a42 * k2 + a43 * k3)));
         PCK_PH(2, (k4 = grp_solve<NSP, G>(x, F, keep * (fu + ih * (C41 * k1 + C42 * k2 + C43 * k3)))));
         u = y + a51 * k1 + a52 * k2 + a53 * k3 + a54 * k4;
-        PCK_PH(3, (fu = grp_rhs<NSP, G, CLAMP>(gv, x, u)));
+        PCK_PH(3, (fu = grp_rhs<NSP, G, CLAMP, Net>(gv, x, u)));
         PCK_PH(2, (k5 = grp_solve<NSP, G>(x, F, keep * (fu + ih * (C51 * k1 + C52 * k2 + C53 * k3 + C54 * k4)))));
         double d2 = 0.0, d3 = 0.0;                 // dense output (mk_solver.h: rodas4_dense)
         if constexpr (TRAJ) {
@@ -859,7 +1019,7 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
             d3 = D31 * k1 + D32 * k2 + D33 * k3 + D34 * k4 + D35 * k5;
         }
         u += k5;
-        PCK_PH(3, (fu = grp_rhs<NSP, G, CLAMP>(gv, x, u)));
+        PCK_PH(3, (fu = grp_rhs<NSP, G, CLAMP, Net>(gv, x, u)));
         PCK_PH(2, (k6 = grp_solve<NSP, G>(x, F, keep * (fu + ih * (C61 * k1 + C62 * k2 + C63 * k3 + C64 * k4 +
                                                                      C65 * k5)))));
         u += k6;
@@ -913,12 +1073,12 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
                             y_old * s1 + sv * (y + s1 * (d2 + sv * d3));
                 }
             }
-            PCK_PH(3, (F0 = grp_rhs<NSP, G, CLAMP>(gv, x, y)));
+            PCK_PH(3, (F0 = grp_rhs<NSP, G, CLAMP, Net>(gv, x, y)));
             // falling tolerance-level negatives to 0 (mk_solver.h: integrate)
             const bool negf = x.row && y < 0.0 && F0 < 0.0;
             if (PCK_POSITIVITY && !CLAMP && gmaxi<G>(negf ? 1 : 0) > 0) {
                 if (negf) y = 0.0;
-                PCK_PH(3, (F0 = grp_rhs<NSP, G, CLAMP>(gv, x, y)));
+                PCK_PH(3, (F0 = grp_rhs<NSP, G, CLAMP, Net>(gv, x, y)));
             }
             h *= fmin(6.0, fmax(0.2, fac));
         } else if (q <= 1.0) {
@@ -959,9 +1119,16 @@ __device__ __forceinline__ double rec_gross(const uint4& rec, double a, double b
 
 // mk_solver.h: imbalance -- the largest |f_i| / gross_i over the rows that are
 // not conservation pivots (group-uniform); f = the row's rate (grp_rhs)
-template <int NSP, int G>
+template <int NSP, int G, class Net = NoNet>
 __device__ __forceinline__ double grp_imbalance(const NetView& nv, const GrpView& g, const Grp<NSP>& x, double y,
                                                 double& f) {
+    if constexpr (IsCt<Net>::v) {
+        double gr = 0.0;
+        f = ct_rhs<Net, NSP, G, false, true>(x, y, &gr);
+        bool pv = false;
+        for (int l = 0; l < nv.NCONS; ++l) pv = pv || (nv.cpiv[l] == x.gl);
+        return gmax<G>((x.row && !pv && f != 0.0) ? fabs(f) / gr : 0.0);
+    }
     f = grp_rhs<NSP, G>(g, x, y);
     wsync();                                   // the rows' reads of the net rates are done
     for (int r = x.gl; r < x.R; r += G) x.d[r] = rec_gross(g.rx[r], x.kf[r], x.kr[r], x.c);
@@ -979,14 +1146,14 @@ __device__ __forceinline__ double grp_imbalance(const NetView& nv, const GrpView
     return gmax<G>((x.row && !pv && f != 0.0) ? fabs(f) / gr : 0.0);
 }
 
-template <int NSP, int G>
+template <int NSP, int G, class Net = NoNet>
 __device__ __forceinline__ bool grp_resolved(const NetView& nv, const GrpView& g, const Grp<NSP>& x, double y) {
     double f;
-    return grp_imbalance<NSP, G>(nv, g, x, y, f) <= PCK_BALANCE_TOL;
+    return grp_imbalance<NSP, G, Net>(nv, g, x, y, f) <= PCK_BALANCE_TOL;
 }
 
 // Newton steady-state polish (same rules as mk_solver.h: newton)
-template <int NSP, int G, int P>
+template <int NSP, int G, int P, class Net = NoNet>
 __device__ __forceinline__ int grp_newton(const NetView& nv, const GrpView& gv, const Grp<NSP>& x, double& y,
                                           int iters, LU<NSP>& F, double dist, double atol) {
     const int NS = x.NS;
@@ -1007,11 +1174,11 @@ __device__ __forceinline__ int grp_newton(const NetView& nv, const GrpView& gv, 
     for (int it = 0; it < iters; ++it) {
         double Gv;
         // the rounding floor (mk_solver.h: PCK_BALANCE_CONV)
-        const double bal = grp_imbalance<NSP, G>(nv, gv, x, z, Gv);
+        const double bal = grp_imbalance<NSP, G, Net>(nv, gv, x, z, Gv);
         if (it >= 2 && bal_prev <= PCK_BALANCE_CONV && bal > bal_prev) { z = z_prev; conv = true; break; }
         bal_prev = bal;
         z_prev = z;
-        grp_jac<NSP, G, P>(nv, gv, x, z, 1.0, 0.0, F.W);
+        grp_jac<NSP, G, P, false, Net>(nv, gv, x, z, 1.0, 0.0, F.W);
 #pragma unroll
         for (int l = 0; l < PCK_MAX_CONS; ++l) {
             if (l < nv.NCONS) {
@@ -1053,7 +1220,7 @@ __device__ __forceinline__ int grp_newton(const NetView& nv, const GrpView& gv, 
     }
     if (!conv) return PCK_ST_NEWTON;
     if (gmin<G>((x.row && z < 0.0) ? -1.0 : 1.0) < 0.0) return PCK_ST_NEWTON;
-    if (!grp_resolved<NSP, G>(nv, gv, x, z)) return PCK_ST_NEWTON;   // converged in absolute terms only
+    if (!grp_resolved<NSP, G, Net>(nv, gv, x, z)) return PCK_ST_NEWTON;   // converged in absolute terms only
     // mk_solver.h: newton -- the root only if the transient end reached it
     if (dist > 0.0 && gmin<G>((x.row && !(fabs(z - y) <= dist * fabs(z) + atol)) ? -1.0 : 1.0) < 0.0)
         return PCK_ST_NEWTON;
@@ -1149,7 +1316,7 @@ struct GrpArgs {
 #ifndef PCK_GRP_WAVES16
 #define PCK_GRP_WAVES16 1
 #endif
-template <int NSP, int G, int P, bool TRAJ = false, bool TAB = false>
+template <int NSP, int G, int P, bool TRAJ = false, bool TAB = false, class Net = NoNet>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 64 ? PCK_GRP_WAVES : PCK_GRP_WAVES16))) k_solve_grp(NetView nv, GrpView gv, CondView cv, const double* kf,
                                                   const double* kr, int64_t ld_k, SolveArgs a, GrpArgs ga) {
     extern __shared__ double lds[];
@@ -1191,9 +1358,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 64
     // transient and polish (a degenerate root's retry transient is a second
     // launch over the compacted list, mk_solver.h: SolveArgs::idx)
     y = x.row ? cv.y0[x.gl * cv.ld_y0 + c * cv.s_y0] : 0.0;
-    int st = grp_integrate<NSP, G, P, TRAJ>(nv, gl, x, y, a.t0, a.t_end, a.rtol, a.atol, a.max_steps, ns,
-                                            a.cons_rows != 0, to, F);
-    if (st == PCK_ST_OK && a.newton) st = grp_newton<NSP, G, P>(nv, gl, x, y, a.newton_iters, F, a.root_dist, a.atol);
+    int st = grp_integrate<NSP, G, P, TRAJ, Net>(nv, gl, x, y, a.t0, a.t_end, a.rtol, a.atol, a.max_steps, ns,
+                                                 a.cons_rows != 0, to, F);
+    if (st == PCK_ST_OK && a.newton)
+        st = grp_newton<NSP, G, P, Net>(nv, gl, x, y, a.newton_iters, F, a.root_dist, a.atol);
     const double tof = grp_tof<NSP, G>(nv, gl, x, y);
     const bool fin = gmin<G>((!x.row || isfinite(y)) ? 1.0 : 0.0) > 0.0 && isfinite(tof);
     if (!fin && st == PCK_ST_OK) st = PCK_ST_NONFINITE;

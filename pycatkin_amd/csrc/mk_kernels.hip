@@ -38,10 +38,12 @@ struct pck_network {
     int plan_mode = PCK_PLAN_AUTO;  // pck_network_set_plan_mode
     unsigned long long digest = 0;
     std::string jit_src;            // mk_jit.h: constexpr plan source for hipRTC (lane networks without a compiled plan)
+    std::string jit_grp_src;        // the same tables for the lane-group solver's compile-time network (mk_group.h: ct_rhs)
     // diagnostics of the last solve (pck_network_dims), the only fields a solve
     // writes: atomic, so calls from several host threads stay race-free
     mutable std::atomic<bool> jit_on{false};      // the last lane solve ran the hipRTC-compiled plan
     mutable std::atomic<bool> grp_jit_on{false};  // the last lane-group solve ran the exact-size hipRTC kernel
+    mutable std::atomic<bool> grp_ct_on{false};   // ... with the network compiled in (mk_group.h: ct_rhs)
 };
 
 // FNV-1a 64 over the solver-side structure (network.py: structural_digest)
@@ -422,6 +424,12 @@ extern "C" int pck_network_create(const int32_t* ip, int64_t n_ip, const double*
         if (nv.NDYN >= 1 && nv.NDYN <= PCK_MAX_DYN_LANE)        // hipRTC plan (also for trajectory solves)
             net->jit_src = jit_source(nv.NDYN, nv.NRXN, nv.NCONS, ip + oef, ip + oer, dp + doff[PCK_D_STOICH],
                                       dp + doff[PCK_D_DYN], dp + doff[PCK_D_CONS], ip + ocp);
+        if (nv.NDYN >= 1 && net->grp_ok)
+            net->jit_grp_src = nv.NDYN <= PCK_MAX_DYN_LANE
+                                   ? net->jit_src
+                                   : jit_source(nv.NDYN, nv.NRXN, nv.NCONS, ip + oef, ip + oer,
+                                                dp + doff[PCK_D_STOICH], dp + doff[PCK_D_DYN], dp + doff[PCK_D_CONS],
+                                                ip + ocp);
     }
     *out = net;
     return PCK_OK;
@@ -440,6 +448,7 @@ extern "C" int pck_network_dims(const pck_network* net, int32_t* dims) {
     dims[0] = v.D; dims[1] = v.NTH; dims[2] = v.NREG; dims[3] = v.NRXN; dims[4] = v.NDYN;
     dims[5] = v.NFIX; dims[6] = v.NCONS; dims[7] = v.NTOF; dims[8] = v.nfeat;
     dims[9] = net->spec ? net->spec : net->jit_on.load(std::memory_order_relaxed) ? PCK_SPEC_JIT : 0;
+    dims[10] = net->grp_ct_on.load(std::memory_order_relaxed) ? 2 : net->grp_jit_on.load(std::memory_order_relaxed) ? 1 : 0;
     return PCK_OK;
 }
 
@@ -852,7 +861,14 @@ static int run_solver(const pck_network* net, const pck_conditions* cond, const 
         int P = grp_p(NS);
         int degmax = 0;
         const int bal = net->gv.LS > 0 ? 1 : 0;
-        if ((net->plan_mode != PCK_PLAN_RUNTIME || traj) && jit_enabled()) {
+        bool ct = false;
+        if ((net->plan_mode != PCK_PLAN_RUNTIME || traj) && jit_enabled() && grp_ct_enabled(G) &&
+            !net->jit_grp_src.empty() && P == 1) {
+            // the compile-time network (mk_group.h: ct_rhs / ct_jac)
+            f = jit_group_ct_kernel(net->digest, net->jit_grp_src, NS, G, P, traj, net->grp_npmax, net->grp_emax);
+            ct = f != nullptr;
+        }
+        if (!ct && (net->plan_mode != PCK_PLAN_RUNTIME || traj) && jit_enabled()) {
             f = jit_group_kernel(NS, G, P, traj, false, net->grp_npmax, net->grp_emax, 0, bal);
             // uniform row loops bounded by the largest row degree (PCK_GRP_DEGMAX):
             // an A/B option (PCK_GRP_DEGMAX=1), taken only where they keep the
@@ -873,7 +889,7 @@ static int run_solver(const pck_network* net, const pck_conditions* cond, const 
             size_t shm_t;
             int qb_t;
             const char* et = getenv("PCK_GRP_TAB");              // A/B: 0 = tables stay in global memory
-            if (!(et && et[0] == '0') && grp_shape(net, NS, P, &shm_t, &qb_t, true) == PCK_OK &&
+            if (!ct && !(et && et[0] == '0') && grp_shape(net, NS, P, &shm_t, &qb_t, true) == PCK_OK &&
                 grp_tables_pay(f, shm, shm_t)) {
                 hipFunction_t ft = jit_group_kernel(NS, G, P, traj, true, net->grp_npmax, net->grp_emax, degmax, bal);
                 if (ft) { f = ft; shm = shm_t; }
@@ -894,6 +910,7 @@ static int run_solver(const pck_network* net, const pck_conditions* cond, const 
 #undef CALL
         }
         net->grp_jit_on.store(f != nullptr, std::memory_order_relaxed);
+        net->grp_ct_on.store(ct, std::memory_order_relaxed);
         HIPCHK(hipGetLastError());
         return PCK_OK;
     }

@@ -42,17 +42,25 @@ class DeviceNetwork:
         L.check(self.lib.pck_network_create(self._ip.ctypes.data_as(C.c_void_p), self._ip.size,
                                             self._dp.ctypes.data_as(C.c_void_p), self._dp.size, C.byref(h)))
         self.h = h
-        dims = (C.c_int32 * 10)()
+        dims = (C.c_int32 * 11)()
         L.check(self.lib.pck_network_dims(self.h, dims))
         (self.D, self.NTH, self.NREG, self.NRXN, self.NDYN, self.NFIX, self.NCONS, self.NTOF,
-         self.nfeat, self.compiled_plan) = list(dims)
+         self.nfeat, self.compiled_plan) = list(dims)[:10]
 
     def plan_id(self):
         """Solver plan of the last lane solve: a compiled-in id (csrc/networks.h),
         100 = hipRTC-specialised at run time (csrc/mk_jit.h), 0 = runtime plan."""
-        dims = (C.c_int32 * 10)()
+        dims = (C.c_int32 * 11)()
         L.check(self.lib.pck_network_dims(self.h, dims))
         return int(dims[9])
+
+    def group_kernel(self):
+        """Kernel of the last lane-group solve: 0 compiled-in record tables,
+        1 hipRTC exact-size record tables, 2 hipRTC with the network compiled
+        in (mk_group.h: ct_rhs / ct_jac)."""
+        dims = (C.c_int32 * 11)()
+        L.check(self.lib.pck_network_dims(self.h, dims))
+        return int(dims[10])
 
     def set_plan_mode(self, mode):
         """A/B switch: 0 / False = auto, 1 / True = runtime plan (never the

@@ -340,19 +340,67 @@ def test_group_exact_size_kernel_matches_compiled(P, inputs, monkeypatch):
     (k_solve_grp<11, 16, 1> for DMTM) and the compiled-in padded kernel
     (k_solve_grp<16, 16, 1>, PCK_JIT=0) do the same arithmetic in the same
     order: bitwise-equal states, TOFs and step counts.  Two runs of the same
-    launch are bitwise equal too (no cross-lane atomics in the sums)."""
+    launch are bitwise equal too (no cross-lane atomics in the sums).  Both
+    are the record-table kernels (PCK_GRP_CT=0; the compile-time network is
+    checked against them in test_group_compile_time_network_matches_tables)."""
     s = _dmtm(P, inputs)
     T = np.linspace(400.0, 800.0, 64)
     kw = dict(T=T, tof_terms=('r5', 'r9'), steady=True)
+    monkeypatch.setenv('PCK_GRP_CT', '0')
     a = s.solve_batch(**kw)
+    assert s.device(('r5', 'r9')).group_kernel() == 1
     b = s.solve_batch(**kw)
     monkeypatch.setenv('PCK_JIT', '0')
     c = s.solve_batch(**kw)
+    assert s.device(('r5', 'r9')).group_kernel() == 0
     monkeypatch.delenv('PCK_JIT')
+    monkeypatch.delenv('PCK_GRP_CT')
     for k in ('y', 'tof', 'status', 'nsteps'):
         np.testing.assert_array_equal(a[k], b[k])
         np.testing.assert_array_equal(a[k], c[k])
     assert np.all(a['status'] == 0)
+
+
+@pytest.mark.parametrize('which', ['dmtm', 'ch4', 'dmtm_drc'])
+def test_group_compile_time_network_matches_tables(P, inputs, monkeypatch, which):
+    """The lane-group solver with the network compiled in (hipRTC, mk_group.h:
+    ct_rhs / ct_jac: every lane evaluates every reaction in straight-line
+    code) against the record-table kernel of the same size (PCK_GRP_CT=0):
+    the same statuses, states and TOFs to rounding -- the two sum the same
+    terms in a different order.  DMTM steady states over T, the CH4 transient
+    (SteadyStateSolver's rtol 1e-10 / atol 1e-12) and the DMTM transient DRC."""
+    if which == 'ch4':
+        s = _ch4(P, inputs)
+        net = s.device()
+        kw = dict(T=np.linspace(473.0, 573.0, 256), t0=0.0, t_end=1e4, rtol=1e-10, atol=1e-12)
+        run = lambda: s.solve_batch(**kw)
+        tol = 1e-7
+    elif which == 'dmtm':
+        s = _dmtm(P, inputs)
+        net = s.device(('r5', 'r9'))
+        run = lambda: s.solve_batch(T=np.linspace(400.0, 800.0, 256), tof_terms=('r5', 'r9'), steady=True)
+        tol = 1e-9
+    else:
+        s = _dmtm(P, inputs)
+        net = s.device(('r5', 'r9'))
+        run = lambda: s.drc_batch(('r5', 'r9'), T=np.linspace(400.0, 800.0, 64), eps=5.0e-2)
+        tol = 1e-5
+    a = run()
+    assert net.group_kernel() == 2
+    monkeypatch.setenv('PCK_GRP_CT', '0')
+    b = run()
+    assert net.group_kernel() == 1
+    monkeypatch.delenv('PCK_GRP_CT')
+    np.testing.assert_array_equal(a['status'], b['status'])
+    assert np.all(a['status'] == 0), np.unique(a['status'], return_counts=True)
+    if which == 'dmtm_drc':
+        for name in s.reactions:
+            np.testing.assert_allclose(a[name], b[name], rtol=0, atol=tol)
+        np.testing.assert_allclose(a['tof0'], b['tof0'], rtol=1e-9)
+        return
+    assert close(a['y'], b['y'], rtol=tol, floor=1e-14), np.abs(a['y'] - b['y']).max()
+    if which != 'ch4':
+        np.testing.assert_allclose(a['tof'], b['tof'], rtol=tol)
 
 
 def test_dmtm_pressure_sweep_vs_oracle(P, inputs):
