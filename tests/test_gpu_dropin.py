@@ -296,3 +296,45 @@ def test_reference_test_1_steps_4_5_7(P, inputs, tmp_path):
             for col, key in (('dEr (J/mol)', 'dErxn'), ('dGr (J/mol)', 'dGrxn'), ('dEa (J/mol)', 'dEa_fwd'),
                              ('dGa (J/mol)', 'dGa_fwd')):
                 np.testing.assert_allclose(dfr[col][k], e[key], rtol=1e-10, atol=1e-6)
+
+
+def _not_reached_node(P, inputs):
+    """A fixture node deep in the O-poisoned corner whose transient has not
+    reached a steady state at t_end (status 4), set up as cooxvolcano.py:28-44."""
+    from pycatkin_amd.functions.volcano import set_volcano_energies
+    fx = np.load(os.path.join(GOLDEN, 'volcano_fixture.npz'))
+    lo, hi, G = fx['grid']
+    be = np.linspace(lo, hi, int(G))
+    cand = np.nonzero(~fx['regular'] & fx['tight_ok'])[0]
+    k = int(cand[np.argmax(be[fx['i'][cand]] - be[fx['j'][cand]])])
+    s = P.read_from_input_file(os.path.join(inputs, 'COOxVolcano', 'input.json'))
+    set_volcano_energies(s)
+    return s, float(be[fx['i'][k]]), float(be[fx['j'][k]])
+
+
+def test_drc_at_a_not_reached_node(P, inputs):
+    """degree_of_rate_control(ss_solve=True) at a node whose transient has not
+    reached a steady state returns its xi, as the reference's does (it never
+    raises on least_squares' answer): every one of the 2R+1 solves reports by
+    the steady rule, and the batch's status says 4."""
+    s, eco, eo = _not_reached_node(P, inputs)
+    d = s.drc_batch(('CO_ox',), T=[600.0], desc={'ECO': [eco], 'EO': [eo]}, eps=1e-3, steady=True)
+    assert d['status'][0] == 4, d['status']
+    assert all(np.isfinite(d[name][0]) for name in s.reactions)
+    assert np.isfinite(d['tof0'][0]) and d['tof0'][0] > 0
+
+
+def test_trajectory_untouched_by_a_retry_pass(P, inputs):
+    """solve_batch(steady=True, t_out=..., retry=...): the optional second
+    launch over the status-4 conditions re-integrates their end state but never
+    writes trajectory samples (a failed retry keeps the first pass's outputs,
+    and a partly rewritten trajectory would mix the two -- ADVICE r3): the
+    trajectory equals the one of the same solve without the retry."""
+    s, eco, eo = _not_reached_node(P, inputs)
+    t_out = np.concatenate([[0.0], np.logspace(-6, np.log10(3600.0), 40)])
+    kw = dict(T=[600.0], desc={'ECO': [eco], 'EO': [eo]}, tof_terms=('CO_ox',), steady=True, t_out=t_out)
+    a = s.solve_batch(**kw)
+    b = s.solve_batch(retry=(1e-8, 1e-22), **kw)
+    assert a['status'][0] == 4 and b['status'][0] in (4, 5)
+    np.testing.assert_array_equal(a['traj'], b['traj'])
+    assert not np.array_equal(a['y'], b['y'])       # the retry did re-integrate the end state

@@ -37,3 +37,13 @@ def test_ts_energies_are_above_both_ends():
             e = ts['TS%d' % j]
             assert e >= sum(E[s] for s in reac) + 0.4 - 1e-12
             assert e >= sum(E[s] for s in prod) + 0.4 - 1e-12
+
+
+def test_presets_accept_every_reported_steady_status():
+    """presets.run_temperatures / run_parameters accept statuses 0 (steady
+    state reached), 4 (transient end reported) and 5 (the same after a failed
+    retry pass) and flag only the integrator failures 1-3."""
+    from pycatkin_amd.functions.presets import _failed
+    st = np.array([0, 4, 5, 1, 2, 3, 0, 5], np.int32)
+    assert _failed(st).tolist() == [3, 4, 5]
+    assert _failed(np.array([0, 4, 5])).size == 0
