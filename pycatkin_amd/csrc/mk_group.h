@@ -391,7 +391,20 @@ struct NoNet {};
 template <class Net> struct IsCt { static constexpr bool v = true; };
 template <> struct IsCt<NoNet> { static constexpr bool v = false; };
 
-// lane q of the calling lane's group, q a compile-time constant after unrolling
+// compile-time loops: body(IC<k>{}) for k = B .. E-1, every index a constant
+// expression (the #pragma unroll of a 58- or 150-reaction loop around an
+// unrolled body gives up past LLVM's unroll threshold and leaves the table
+// lookups and their branches at run time)
+template <int V> struct IC { static constexpr int value = V; };
+template <int B, int E, class F>
+__device__ __forceinline__ void sfor(F&& body) {
+    if constexpr (B < E) {
+        body(IC<B>{});
+        sfor<B + 1, E>(body);
+    }
+}
+
+// lane q of the calling lane's group, q a compile-time constant
 template <int G>
 __device__ __forceinline__ double gbcast_k(double v, int q) {
     if constexpr (G == 16) {
@@ -409,120 +422,170 @@ __device__ __forceinline__ double gbcast_k(double v, int q) {
 #ifndef PCK_CT_ACC_MAX
 #define PCK_CT_ACC_MAX 24
 #endif
+// Straight-line code over every reaction lets the scheduler hoist all the
+// k_eff loads and products to the top (for CH4: 512 VGPRs, 830 spilled);
+// a scheduling barrier every PCK_CT_CHUNK reactions bounds the live ranges
+// to one chunk (the other waves of the SIMD hide the chunk's LDS latency).
+#ifndef PCK_CT_CHUNK
+#define PCK_CT_CHUNK 4
+#endif
+// the condition's k_eff from LDS, re-read at every evaluation: loop-invariant
+// over the whole solve, LLVM would otherwise hoist all 2R loads out of the
+// step loop and keep them live (CH4: 232 VGPRs)
+typedef __attribute__((address_space(3))) const double lds_cdouble;
+__device__ __forceinline__ double ct_k(const double* p, int j) { return ((lds_cdouble*)p)[j]; }
+// an evaluation starts with a compiler memory barrier: the k_eff loads below
+// it cannot be hoisted out of the step loop (no instruction is emitted)
+__device__ __forceinline__ void ct_reload() { asm volatile("" ::: "memory"); }
+// At a chunk boundary the running sums pass through an empty asm: volatile
+// asm statements keep their order, so every value a chunk computes is
+// finished before the next chunk's loads issue (a memory clobber alone
+// orders the loads but lets the selection-DAG scheduler sink the arithmetic
+// below all of them).
+template <int J, int N>
+__device__ __forceinline__ void ct_fence(double (&v)[N]) {
+    if constexpr ((J + 1) % PCK_CT_CHUNK == 0) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) asm volatile("" : "+v"(v[i]) :: "memory");
+    }
+}
 
 template <class Net, int NSP, int G, bool CL>
 __device__ __forceinline__ void ct_conc(const Grp<NSP>& x, double y, double (&c)[Net::NS]) {
     const double v = (CL && PCK_GRP_CLAMP) ? fmax(y, 0.0) : y;
-#pragma unroll
-    for (int q = 0; q < Net::NS; ++q) c[q] = Net::dyn(q, 0) * gbcast_k<G>(v, q);
+    sfor<0, Net::NS>([&](auto qc) {
+        constexpr int q = decltype(qc)::value;
+        c[q] = Net::dyn(q, 0) * gbcast_k<G>(v, q);
+    });
 }
 
-// S(gl, j): the calling lane's coefficient of column j (0 off its row)
-template <class Net, int NSP>
-__device__ __forceinline__ double ct_coef(const Grp<NSP>& x, int j) {
+// S(gl, j): the calling lane's coefficient of column J (0 off its row)
+template <class Net, int J, int NSP>
+__device__ __forceinline__ double ct_coef(const Grp<NSP>& x) {
     double s = 0.0;
-#pragma unroll
-    for (int i = 0; i < Net::NS; ++i)
-        if (Net::S(i, j) != 0.0) s = (x.gl == i) ? Net::S(i, j) : s;
+    sfor<0, Net::NS>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        if constexpr (Net::S(i, J) != 0.0) s = (x.gl == i) ? Net::S(i, J) : s;
+    });
     return s;
 }
 
-template <class Net>
-__device__ __forceinline__ bool ct_col_used(int j) {
-    bool u = false;
-#pragma unroll
-    for (int i = 0; i < Net::NS; ++i) u = u || (Net::S(i, j) != 0.0);
-    return u;
+template <class Net, int J>
+__device__ __forceinline__ constexpr bool ct_col_used() {
+    for (int i = 0; i < Net::NS; ++i)
+        if (Net::S(i, J) != 0.0) return true;
+    return false;
 }
 
-// forward / reverse rate of reaction j (kf, kr: the condition's effective constants)
-template <class Net>
-__device__ __forceinline__ void ct_rate(int j, double kf, double kr, const double (&c)[Net::NS], double& rf,
-                                        double& rr) {
+// x^E for a compile-time E >= 1
+template <int E>
+__device__ __forceinline__ double cpow(double x) {
+    if constexpr (E == 1) return x;
+    else if constexpr (E == 2) return x * x;
+    else return x * cpow<E - 1>(x);
+}
+
+// forward / reverse rate of reaction J (kf, kr: the condition's effective constants)
+template <class Net, int J>
+__device__ __forceinline__ void ct_rate(double kf, double kr, const double (&c)[Net::NS], double& rf, double& rr) {
     rf = kf;
     rr = kr;
-#pragma unroll
-    for (int i = 0; i < Net::NS; ++i) {
-        if (Net::ef(j, i)) rf *= ipow(c[i], Net::ef(j, i));
-        if (Net::er(j, i)) rr *= ipow(c[i], Net::er(j, i));
-    }
+    sfor<0, Net::NS>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        if constexpr (Net::ef(J, i) > 0) rf *= cpow<Net::ef(J, i)>(c[i]);
+        if constexpr (Net::er(J, i) > 0) rr *= cpow<Net::er(J, i)>(c[i]);
+    });
 }
 
-// f (and with GROSS the gross flux g) of the calling lane's row
+// f (and with GROSS the gross flux) of the calling lane's row
 template <class Net, int NSP, int G, bool CL, bool GROSS = false>
 __device__ __forceinline__ double ct_rhs(const Grp<NSP>& x, double y, double* gross = nullptr) {
     constexpr int NS = Net::NS, R = Net::R;
+    ct_reload();
     double c[NS];
     ct_conc<Net, NSP, G, CL>(x, y, c);
     double f = 0.0, gacc = 0.0;
     if constexpr (NS <= PCK_CT_ACC_MAX && !GROSS) {
         double acc[NS];
-#pragma unroll
-        for (int i = 0; i < NS; ++i) acc[i] = 0.0;
-#pragma unroll
-        for (int j = 0; j < R; ++j) {
-            if (!ct_col_used<Net>(j)) continue;
-            double rf, rr;
-            ct_rate<Net>(j, x.kf[j], x.kr[j], c, rf, rr);
-            const double net = rf - rr;
-#pragma unroll
-            for (int i = 0; i < NS; ++i)
-                if (Net::S(i, j) != 0.0) acc[i] += Net::S(i, j) * net;
-        }
-#pragma unroll
-        for (int i = 0; i < NS; ++i) f = (x.gl == i) ? acc[i] : f;
+        sfor<0, NS>([&](auto ic) { acc[decltype(ic)::value] = 0.0; });
+        sfor<0, R>([&](auto jc) {
+            constexpr int j = decltype(jc)::value;
+            if constexpr (ct_col_used<Net, j>()) {
+                double rf, rr;
+                ct_rate<Net, j>(ct_k(x.kf, j), ct_k(x.kr, j), c, rf, rr);
+                const double net = rf - rr;
+                sfor<0, NS>([&](auto ic) {
+                    constexpr int i = decltype(ic)::value;
+                    if constexpr (Net::S(i, j) != 0.0) acc[i] += Net::S(i, j) * net;
+                });
+                ct_fence<j>(acc);
+            }
+        });
+        sfor<0, NS>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            f = (x.gl == i) ? acc[i] : f;
+        });
     } else {
-#pragma unroll
-        for (int j = 0; j < R; ++j) {
-            if (!ct_col_used<Net>(j)) continue;
-            double rf, rr;
-            ct_rate<Net>(j, x.kf[j], x.kr[j], c, rf, rr);
-            const double s = ct_coef<Net>(x, j);
-            f = fma(s, rf - rr, f);
-            if constexpr (GROSS) gacc = fma(fabs(s), fabs(rf) + fabs(rr), gacc);
-        }
+        sfor<0, R>([&](auto jc) {
+            constexpr int j = decltype(jc)::value;
+            if constexpr (ct_col_used<Net, j>()) {
+                double rf, rr;
+                ct_rate<Net, j>(ct_k(x.kf, j), ct_k(x.kr, j), c, rf, rr);
+                const double s = ct_coef<Net, j>(x);
+                f = fma(s, rf - rr, f);
+                if constexpr (GROSS) gacc = fma(fabs(s), fabs(rf) + fabs(rr), gacc);
+                double fg[2] = {f, gacc};
+                ct_fence<j>(fg);
+                f = fg[0];
+                gacc = fg[1];
+            }
+        });
     }
     if (!x.row) return 0.0;
     if constexpr (GROSS) *gross = gacc * fabs(x.rs) + fabs(x.fl) * (fabs(x.in) + fabs(y));
     return f * x.rs + x.fl * (x.in - y);
 }
 
+// d(prod_i c_i^E(J, i)) / d y_Q, times k (mk_solver.h: jac)
+template <class Net, int J, int Q, bool FWD>
+__device__ __forceinline__ double ct_dside(double k, const double (&c)[Net::NS]) {
+    constexpr int eq = FWD ? Net::ef(J, Q) : Net::er(J, Q);
+    double t = k * (double)eq * Net::dyn(Q, 0);
+    if constexpr (eq > 1) t *= cpow<eq - 1>(c[Q]);
+    sfor<0, Net::NS>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        constexpr int ei = FWD ? Net::ef(J, i) : Net::er(J, i);
+        if constexpr (i != Q && ei > 0) t *= cpow<ei>(c[i]);
+    });
+    return t;
+}
+
 // W[q] = sgn * dF_i/dy_q + (q == i ? shift : 0) on the calling lane's row i
 template <class Net, int NSP, int G, bool CL>
 __device__ __forceinline__ void ct_jac(const Grp<NSP>& x, double y, double sgn, double shift, double (&W)[NSP]) {
     constexpr int NS = Net::NS, R = Net::R;
+    ct_reload();
     double c[NS];
     ct_conc<Net, NSP, G, CL>(x, y, c);
     double jr[NS];
-#pragma unroll
-    for (int q = 0; q < NS; ++q) jr[q] = 0.0;
-#pragma unroll
-    for (int j = 0; j < R; ++j) {
-        if (!ct_col_used<Net>(j)) continue;
-        const double s = ct_coef<Net>(x, j);
-        const double kf = x.kf[j], kr = x.kr[j];
-        // d net_j / d y_q for every participant q (mk_solver.h: jac)
-#pragma unroll
-        for (int q = 0; q < NS; ++q) {
-            if (!(Net::ef(j, q) || Net::er(j, q))) continue;
-            double v = 0.0;
-            if (Net::ef(j, q)) {
-                double t = kf * (double)Net::ef(j, q) * Net::dyn(q, 0) * ipow(c[q], Net::ef(j, q) - 1);
-#pragma unroll
-                for (int i = 0; i < NS; ++i)
-                    if (i != q && Net::ef(j, i)) t *= ipow(c[i], Net::ef(j, i));
-                v += t;
-            }
-            if (Net::er(j, q)) {
-                double t = kr * (double)Net::er(j, q) * Net::dyn(q, 0) * ipow(c[q], Net::er(j, q) - 1);
-#pragma unroll
-                for (int i = 0; i < NS; ++i)
-                    if (i != q && Net::er(j, i)) t *= ipow(c[i], Net::er(j, i));
-                v -= t;
-            }
-            jr[q] = fma(s, v, jr[q]);
+    sfor<0, NS>([&](auto qc) { jr[decltype(qc)::value] = 0.0; });
+    sfor<0, R>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        if constexpr (ct_col_used<Net, j>()) {
+            const double s = ct_coef<Net, j>(x);
+            const double kf = ct_k(x.kf, j), kr = ct_k(x.kr, j);
+            sfor<0, NS>([&](auto qc) {
+                constexpr int q = decltype(qc)::value;
+                if constexpr (Net::ef(j, q) > 0 || Net::er(j, q) > 0) {
+                    double v = 0.0;
+                    if constexpr (Net::ef(j, q) > 0) v += ct_dside<Net, j, q, true>(kf, c);
+                    if constexpr (Net::er(j, q) > 0) v -= ct_dside<Net, j, q, false>(kr, c);
+                    jr[q] = fma(s, v, jr[q]);
+                }
+            });
+            ct_fence<j>(jr);
         }
-    }
+    });
     const double sc = sgn * x.rs;
     const double dg = shift - sgn * x.fl;
 #pragma unroll
@@ -1002,6 +1065,36 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
             continue;
         }
         double k1, k2, k3, k4, k5, k6, fu, u;
+        if constexpr (IsCt<Net>::v) {
+            // the straight-line network code is large: one rhs and one solve
+            // site for the five stages (the same stage formulas, unused
+            // coefficients zero; u_6 = u_5 + k5 as a sixth row)
+            PCK_PH(2, (k1 = grp_solve<NSP, G>(x, F, keep * F0)));
+            k2 = k3 = k4 = k5 = k6 = 0.0;
+#pragma unroll 1
+            for (int st = 2; st <= 6; ++st) {
+                double b1, b2, b3, b4, b5, e1, e2, e3, e4, e5;
+                switch (st) {
+                    case 2: b1 = a21; b2 = b3 = b4 = b5 = 0.0; e1 = C21; e2 = e3 = e4 = e5 = 0.0; break;
+                    case 3: b1 = a31; b2 = a32; b3 = b4 = b5 = 0.0; e1 = C31; e2 = C32; e3 = e4 = e5 = 0.0; break;
+                    case 4: b1 = a41; b2 = a42; b3 = a43; b4 = b5 = 0.0; e1 = C41; e2 = C42; e3 = C43; e4 = e5 = 0.0; break;
+                    case 5: b1 = a51; b2 = a52; b3 = a53; b4 = a54; b5 = 0.0; e1 = C51; e2 = C52; e3 = C53; e4 = C54;
+                            e5 = 0.0; break;
+                    default: b1 = a51; b2 = a52; b3 = a53; b4 = a54; b5 = 1.0; e1 = C61; e2 = C62; e3 = C63; e4 = C64;
+                             e5 = C65; break;
+                }
+                u = y + b1 * k1 + b2 * k2 + b3 * k3 + b4 * k4 + b5 * k5;
+                PCK_PH(3, (fu = grp_rhs<NSP, G, CLAMP, Net>(gv, x, u)));
+                double kn;
+                PCK_PH(2, (kn = grp_solve<NSP, G>(x, F, keep * (fu + ih * (e1 * k1 + e2 * k2 + e3 * k3 + e4 * k4 +
+                                                                           e5 * k5)))));
+                k2 = (st == 2) ? kn : k2;
+                k3 = (st == 3) ? kn : k3;
+                k4 = (st == 4) ? kn : k4;
+                k5 = (st == 5) ? kn : k5;
+                k6 = (st == 6) ? kn : k6;
+            }
+        } else {
         PCK_PH(2, (k1 = grp_solve<NSP, G>(x, F, keep * F0)));
         PCK_PH(3, (fu = grp_rhs<NSP, G, CLAMP, Net>(gv, x, y + a21 * k1)));
         PCK_PH(2, (k2 = grp_solve<NSP, G>(x, F, keep * (fu + ih * (C21 * k1)))));
@@ -1012,16 +1105,17 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
         u = y + a51 * k1 + a52 * k2 + a53 * k3 + a54 * k4;
         PCK_PH(3, (fu = grp_rhs<NSP, G, CLAMP, Net>(gv, x, u)));
         PCK_PH(2, (k5 = grp_solve<NSP, G>(x, F, keep * (fu + ih * (C51 * k1 + C52 * k2 + C53 * k3 + C54 * k4)))));
+        u += k5;
+        PCK_PH(3, (fu = grp_rhs<NSP, G, CLAMP, Net>(gv, x, u)));
+        PCK_PH(2, (k6 = grp_solve<NSP, G>(x, F, keep * (fu + ih * (C61 * k1 + C62 * k2 + C63 * k3 + C64 * k4 +
+                                                                     C65 * k5)))));
+        }
         double d2 = 0.0, d3 = 0.0;                 // dense output (mk_solver.h: rodas4_dense)
         if constexpr (TRAJ) {
             using namespace rodas4_dense;
             d2 = D21 * k1 + D22 * k2 + D23 * k3 + D24 * k4 + D25 * k5;
             d3 = D31 * k1 + D32 * k2 + D33 * k3 + D34 * k4 + D35 * k5;
         }
-        u += k5;
-        PCK_PH(3, (fu = grp_rhs<NSP, G, CLAMP, Net>(gv, x, u)));
-        PCK_PH(2, (k6 = grp_solve<NSP, G>(x, F, keep * (fu + ih * (C61 * k1 + C62 * k2 + C63 * k3 + C64 * k4 +
-                                                                     C65 * k5)))));
         u += k6;
         const double sc = atol + rtol * fmax(fabs(y), fabs(u));
         const double r = k6 * __builtin_amdgcn_rcp(sc);     // error weight: the v_rcp_f64 estimate suffices

@@ -370,7 +370,7 @@ def test_group_compile_time_network_matches_tables(P, inputs, monkeypatch, which
     terms in a different order.  DMTM steady states over T, the CH4 transient
     (SteadyStateSolver's rtol 1e-10 / atol 1e-12) and the DMTM transient DRC."""
     if which == 'ch4':
-        s = _ch4(P, inputs)
+        s, _ = _ch4(P, inputs)
         net = s.device()
         kw = dict(T=np.linspace(473.0, 573.0, 256), t0=0.0, t_end=1e4, rtol=1e-10, atol=1e-12)
         run = lambda: s.solve_batch(**kw)
@@ -396,7 +396,9 @@ def test_group_compile_time_network_matches_tables(P, inputs, monkeypatch, which
     if which == 'dmtm_drc':
         for name in s.reactions:
             np.testing.assert_allclose(a[name], b[name], rtol=0, atol=tol)
-        np.testing.assert_allclose(a['tof0'], b['tof0'], rtol=1e-9)
+        # transients at the input's rtol 1e-6: rounding moves the step sequence
+        # (measured 3.5e-8 relative on the base TOF)
+        np.testing.assert_allclose(a['tof0'], b['tof0'], rtol=1e-6)
         return
     assert close(a['y'], b['y'], rtol=tol, floor=1e-14), np.abs(a['y'] - b['y']).max()
     if which != 'ch4':

@@ -40,8 +40,11 @@ def shard_ms(bench, torch, scaling, rank, world, steps, extra=()):
         ts.append(a.elapsed_time(b))
     st = wl.status().cpu().numpy()
     ns = wl.nsteps().cpu().numpy().astype(np.int64)
+    pad = (-ns.size) % 64
+    waves = np.concatenate([ns, np.zeros(pad, ns.dtype)]).reshape(-1, 64).max(axis=1)
     return dict(rank=rank, ms=float(np.median(ts)), units=int(wl.n_local), steps_max=int(ns.max()),
-                steps_mean=float(ns.mean()), degenerate=int((st == 4).sum()))
+                steps_mean=float(ns.mean()), lane_eff=float(ns.mean() / waves.mean()),
+                wave_steps_p99=float(np.percentile(waves, 99)), degenerate=int((st == 4).sum()))
 
 
 def main():
