@@ -52,9 +52,9 @@ def main():
     ap.add_argument('--steps', type=int, default=3)
     ap.add_argument('--worlds', default='1,2,4,8', help='strong-scaling world sizes')
     ap.add_argument('--no-weak', action='store_true')
-    ap.add_argument('--bench-args', default='', help="extra bench.py arguments, ','-separated (A/B)")
+    ap.add_argument('--bench-args', default='', help="extra bench.py arguments, '+'-separated (A/B)")
     a = ap.parse_args()
-    extra = [x for x in a.bench_args.split(',') if x]
+    extra = [x for x in a.bench_args.split('+') if x]
     import torch
     import bench
     out = []
