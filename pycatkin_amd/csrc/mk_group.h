@@ -459,13 +459,21 @@ __device__ __forceinline__ void ct_conc(const Grp<NSP>& x, double y, double (&c)
     });
 }
 
-// S(gl, j): the calling lane's coefficient of column J (0 off its row)
-template <class Net, int J, int NSP>
-__device__ __forceinline__ double ct_coef(const Grp<NSP>& x) {
+// S(gl, j): the calling lane's coefficient of column J (0 off its row).  gl
+// is the lane's row as returned by ct_row(): the coefficients only depend on
+// it, so LLVM would hoist all R of them out of the step loop and keep them
+// live (CH4: 116 VGPRs, one wave per SIMD); ct_row() hides gl behind an
+// empty asm at every evaluation, so they are recomputed (a few selects each).
+__device__ __forceinline__ int ct_row(int gl) {
+    asm volatile("" : "+v"(gl));
+    return gl;
+}
+template <class Net, int J>
+__device__ __forceinline__ double ct_coef(int gl) {
     double s = 0.0;
     sfor<0, Net::NS>([&](auto ic) {
         constexpr int i = decltype(ic)::value;
-        if constexpr (Net::S(i, J) != 0.0) s = (x.gl == i) ? Net::S(i, J) : s;
+        if constexpr (Net::S(i, J) != 0.0) s = (gl == i) ? Net::S(i, J) : s;
     });
     return s;
 }
@@ -502,6 +510,7 @@ template <class Net, int NSP, int G, bool CL, bool GROSS = false>
 __device__ __forceinline__ double ct_rhs(const Grp<NSP>& x, double y, double* gross = nullptr) {
     constexpr int NS = Net::NS, R = Net::R;
     ct_reload();
+    const int gl = ct_row(x.gl);
     double c[NS];
     ct_conc<Net, NSP, G, CL>(x, y, c);
     double f = 0.0, gacc = 0.0;
@@ -523,7 +532,7 @@ __device__ __forceinline__ double ct_rhs(const Grp<NSP>& x, double y, double* gr
         });
         sfor<0, NS>([&](auto ic) {
             constexpr int i = decltype(ic)::value;
-            f = (x.gl == i) ? acc[i] : f;
+            f = (gl == i) ? acc[i] : f;
         });
     } else {
         sfor<0, R>([&](auto jc) {
@@ -531,7 +540,7 @@ __device__ __forceinline__ double ct_rhs(const Grp<NSP>& x, double y, double* gr
             if constexpr (ct_col_used<Net, j>()) {
                 double rf, rr;
                 ct_rate<Net, j>(ct_k(x.kf, j), ct_k(x.kr, j), c, rf, rr);
-                const double s = ct_coef<Net, j>(x);
+                const double s = ct_coef<Net, j>(gl);
                 f = fma(s, rf - rr, f);
                 if constexpr (GROSS) gacc = fma(fabs(s), fabs(rf) + fabs(rr), gacc);
                 double fg[2] = {f, gacc};
@@ -565,6 +574,7 @@ template <class Net, int NSP, int G, bool CL>
 __device__ __forceinline__ void ct_jac(const Grp<NSP>& x, double y, double sgn, double shift, double (&W)[NSP]) {
     constexpr int NS = Net::NS, R = Net::R;
     ct_reload();
+    const int gl = ct_row(x.gl);
     double c[NS];
     ct_conc<Net, NSP, G, CL>(x, y, c);
     double jr[NS];
@@ -572,7 +582,7 @@ __device__ __forceinline__ void ct_jac(const Grp<NSP>& x, double y, double sgn, 
     sfor<0, R>([&](auto jc) {
         constexpr int j = decltype(jc)::value;
         if constexpr (ct_col_used<Net, j>()) {
-            const double s = ct_coef<Net, j>(x);
+            const double s = ct_coef<Net, j>(gl);
             const double kf = ct_k(x.kf, j), kr = ct_k(x.kr, j);
             sfor<0, NS>([&](auto qc) {
                 constexpr int q = decltype(qc)::value;
