@@ -503,6 +503,7 @@ class System:
                for name in plan.all_reactions}
         out['tof0'] = r['tof0'].cpu().numpy()
         out['status'] = r['status'].cpu().numpy()
+        out['nsteps'] = r['nsteps'].cpu().numpy()
         return out
 
     # -- reference API (one condition) -------------------------------------------------
