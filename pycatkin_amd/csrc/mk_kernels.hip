@@ -862,7 +862,7 @@ static int run_solver(const pck_network* net, const pck_conditions* cond, const 
         int degmax = 0;
         const int bal = net->gv.LS > 0 ? 1 : 0;
         bool ct = false;
-        if ((net->plan_mode != PCK_PLAN_RUNTIME || traj) && jit_enabled() && grp_ct_enabled(G) &&
+        if ((net->plan_mode != PCK_PLAN_RUNTIME || traj) && jit_enabled() && grp_ct_enabled(G, net->nv.NRXN) &&
             !net->jit_grp_src.empty() && P == 1) {
             // the compile-time network (mk_group.h: ct_rhs / ct_jac)
             f = jit_group_ct_kernel(net->digest, net->jit_grp_src, NS, G, P, traj, net->grp_npmax, net->grp_emax);
