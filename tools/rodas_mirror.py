@@ -212,7 +212,7 @@ def synthetic_model(idx, n_total=65536):
 def dmtm_model(T):
     from oracle import mk_oracle as O
     spec = O.load_spec(os.path.join(ROOT, 'tests', 'golden', 'inputs', 'DMTM', 'input.json'))
-    return O.ClassicModel(spec, T=T), [T]
+    return O.ClassicModel(spec, T=T, p=float(os.environ.get('P', spec['system']['p']))), [T]
 
 
 def main():
