@@ -493,9 +493,18 @@ __device__ __forceinline__ double cpow(double x) {
     else return x * cpow<E - 1>(x);
 }
 
+// rf - rr rounded as written: with contraction the difference would fold one
+// product into an FMA and stop cancelling exactly where the two rates agree
+// (mk_group.h rec_rate keeps contraction off for the same reason)
+__device__ __forceinline__ double ct_sub(double a, double b) {
+#pragma clang fp contract(off)
+    return a - b;
+}
+
 // forward / reverse rate of reaction J (kf, kr: the condition's effective constants)
 template <class Net, int J>
 __device__ __forceinline__ void ct_rate(double kf, double kr, const double (&c)[Net::NS], double& rf, double& rr) {
+#pragma clang fp contract(off)
     rf = kf;
     rr = kr;
     sfor<0, Net::NS>([&](auto ic) {
@@ -522,7 +531,7 @@ __device__ __forceinline__ double ct_rhs(const Grp<NSP>& x, double y, double* gr
             if constexpr (ct_col_used<Net, j>()) {
                 double rf, rr;
                 ct_rate<Net, j>(ct_k(x.kf, j), ct_k(x.kr, j), c, rf, rr);
-                const double net = rf - rr;
+                const double net = ct_sub(rf, rr);
                 sfor<0, NS>([&](auto ic) {
                     constexpr int i = decltype(ic)::value;
                     if constexpr (Net::S(i, j) != 0.0) acc[i] += Net::S(i, j) * net;
@@ -541,7 +550,7 @@ __device__ __forceinline__ double ct_rhs(const Grp<NSP>& x, double y, double* gr
                 double rf, rr;
                 ct_rate<Net, j>(ct_k(x.kf, j), ct_k(x.kr, j), c, rf, rr);
                 const double s = ct_coef<Net, j>(gl);
-                f = fma(s, rf - rr, f);
+                f = fma(s, ct_sub(rf, rr), f);
                 if constexpr (GROSS) gacc = fma(fabs(s), fabs(rf) + fabs(rr), gacc);
                 double fg[2] = {f, gacc};
                 ct_fence<j>(fg);
