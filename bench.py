@@ -447,6 +447,9 @@ def ch4_workload(args, rank, world):
     return wl
 
 
+SYNTHETIC_TOL = (1.0e-7, 1.0e-22)
+
+
 def synthetic_workload(args, rank, world):
     from pycatkin_amd.functions.synthetic import synthetic_system
     wl = Workload()
@@ -457,12 +460,16 @@ def synthetic_workload(args, rank, world):
     rng = np.random.default_rng(0)
     D = _shard(rng.uniform(-0.5, 0.5, (n_tot if args.scaling == 'strong' else n_tot * world, 4)), rank, world)
     n = D.shape[0]
+    # the steady rule's transient at rtol 1e-7: at the default 1e-6 two of the
+    # 324 fixture rows miss the 1e-6 bound against the oracle's rtol 1e-11
+    # transient (profiles/r4/synthetic_tol_probe.jsonl)
     _solve_workload(wl, sim, net, plan, n, np.full(n, 500.0), None, {'D%d' % k: D[:, k] for k in range(4)},
-                    ('R0',), True, False, args=args)
+                    ('R0',), True, False, rtol=SYNTHETIC_TOL[0], atol=SYNTHETIC_TOL[1], args=args)
     wl.kernel_name = 'k_solve_grp<64, 64>'
     wl.tag = 'synthetic %d' % n_tot
     wl.config = {'workload': 'synthetic 50 species / 150 reactions, %d random-descriptor conditions, T=500 K, '
-                             't_end 1e4 s (rtol 1e-8 / atol 1e-10) + Newton steady state' % n_tot,
+                             'transient to t_end 1e4 s at rtol %g / atol %g + Newton, steady rule (root where '
+                             'reached, else the transient end)' % ((n_tot,) + SYNTHETIC_TOL),
                  'parallelism': 'dp%d' % world}
     wl.data = 'synthetic network (functions/synthetic.py), uniform random descriptors in [-0.5, 0.5] eV'
     return wl

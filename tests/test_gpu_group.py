@@ -283,7 +283,8 @@ def test_synthetic_fixture_parity(P, synthetic):
     lsoda at rtol 1e-11 / atol 1e-20).
 
     The fixture rows are solved inside the whole 65 536-condition bench set
-    (one launch, the library's default step budget): every condition ends
+    (one launch at the bench's rtol 1e-7 / atol 1e-22, the library's default
+    step budget): every condition ends
     with status 0 (steady state reached) or 4 (the transient end), the site
     balance holds everywhere, and at the fixture rows
       * log10(TOF of R0) within 1e-6 relative of the oracle's answer (the
@@ -301,8 +302,10 @@ def test_synthetic_fixture_parity(P, synthetic):
     fx = dict(np.load(os.path.join(HERE, 'golden', 'synthetic_fixture.npz')))
     D = np.random.default_rng(0).uniform(-0.5, 0.5, (65536, 4))
     np.testing.assert_array_equal(D[fx['idx']], fx['desc'])
+    # the bench's tolerances (bench.SYNTHETIC_TOL): at the default 1e-6 two of
+    # the 324 rows miss 1e-6 (max 4.4e-6; tools/synthetic_tol_probe.py)
     r = sim.solve_batch(T=np.full(D.shape[0], 500.0), desc={'D%d' % k: D[:, k] for k in range(4)},
-                        tof_terms=('R0',), steady=True)
+                        tof_terms=('R0',), steady=True, rtol=1e-7, atol=1e-22)
     st = r['status']
     counts = {int(k): int(v) for k, v in zip(*np.unique(st, return_counts=True))}
     assert set(counts) <= {0, 4}, counts
