@@ -113,6 +113,21 @@ struct Lane {
 //   f_i = rs_i * sum_j S_ij (kf_j prod c^a - kr_j prod c^b) + fl_i (in_i - y_i),
 //   c_i = cf_i y_i,  rs_i = rs0_i + rsT_i T.
 // ---------------------------------------------------------------------------
+// rf - rr as written (PCK_NET_EXACT=1): with FMA contraction the compiler may
+// fold the last product of rr into the subtraction, and the two rates then no
+// longer cancel exactly where they agree -- on the lane-group kernel that
+// noise turned some 1e12 s DMTM transients into 80x more steps
+// (mk_group.h: ct_sub)
+#ifndef PCK_NET_EXACT
+#define PCK_NET_EXACT 0
+#endif
+__device__ __forceinline__ double net_rate(double rf, double rr) {
+#if PCK_NET_EXACT
+#pragma clang fp contract(off)
+#endif
+    return rf - rr;
+}
+
 template <class P, class K>
 __device__ __forceinline__ void rhs(const P& p, const Lane<P::NS>& L, const K& k, const double (&y)[P::NS],
                                     double (&f)[P::NS]) {
@@ -127,7 +142,7 @@ __device__ __forceinline__ void rhs(const P& p, const Lane<P::NS>& L, const K& k
             if (p.ef(j, i)) rf *= ipow(c[i], p.ef(j, i));
             if (p.er(j, i)) rr *= ipow(c[i], p.er(j, i));
         }
-        const double net = rf - rr;
+        const double net = net_rate(rf, rr);
 #pragma unroll
         for (int i = 0; i < NS; ++i) {
             const double s = p.S(i, j);
@@ -622,7 +637,7 @@ __device__ __forceinline__ void rhs_gross(const P& p, const Lane<P::NS>& L, cons
             if (p.ef(j, i)) rf *= ipow(c[i], p.ef(j, i));
             if (p.er(j, i)) rr *= ipow(c[i], p.er(j, i));
         }
-        const double net = rf - rr, gross = fabs(rf) + fabs(rr);
+        const double net = net_rate(rf, rr), gross = fabs(rf) + fabs(rr);
 #pragma unroll
         for (int i = 0; i < NS; ++i) {
             const double s = p.S(i, j);
