@@ -392,7 +392,6 @@ def test_group_compile_time_network_matches_tables(P, inputs, monkeypatch, which
         net = s.device(('r5', 'r9'))
         run = lambda: s.drc_batch(('r5', 'r9'), T=np.linspace(400.0, 800.0, 64), eps=5.0e-2)
         tol = 1e-5
-    monkeypatch.setenv('PCK_GRP_CT', '1')          # DMTM's default is the table kernel (R <= 2 G)
     a = run()
     assert net.group_kernel() == 2
     monkeypatch.setenv('PCK_GRP_CT', '0')
