@@ -387,6 +387,7 @@ __device__ __forceinline__ void put_c(const Grp<NSP>& x, double y) {
 // The record-table path (above: lane-per-reaction, then the CSR gather) does
 // the same arithmetic in another order: the two agree to rounding.
 // ---------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) const double lds_cdouble;
 struct NoNet {};
 template <class Net> struct IsCt { static constexpr bool v = true; };
 template <> struct IsCt<NoNet> { static constexpr bool v = false; };
@@ -432,7 +433,6 @@ __device__ __forceinline__ double gbcast_k(double v, int q) {
 // the condition's k_eff from LDS, re-read at every evaluation: loop-invariant
 // over the whole solve, LLVM would otherwise hoist all 2R loads out of the
 // step loop and keep them live (CH4: 232 VGPRs)
-typedef __attribute__((address_space(3))) const double lds_cdouble;
 __device__ __forceinline__ double ct_k(const double* p, int j) { return ((lds_cdouble*)p)[j]; }
 // an evaluation starts with a compiler memory barrier: the k_eff loads below
 // it cannot be hoisted out of the step loop (no instruction is emitted)
@@ -452,11 +452,22 @@ __device__ __forceinline__ void ct_fence(double (&v)[N]) {
 
 template <class Net, int NSP, int G, bool CL>
 __device__ __forceinline__ void ct_conc(const Grp<NSP>& x, double y, double (&c)[Net::NS]) {
-    const double v = (CL && PCK_GRP_CLAMP) ? fmax(y, 0.0) : y;
-    sfor<0, Net::NS>([&](auto qc) {
-        constexpr int q = decltype(qc)::value;
-        c[q] = Net::dyn(q, 0) * gbcast_k<G>(v, q);
-    });
+    if constexpr (G == 64) {
+        // a wavefront's group: v_readlane would put all NS concentrations in
+        // SGPRs (NS = 50: 100 of them, ~2 000 spilled); an LDS round trip
+        // gives VGPRs (each read is one broadcast address)
+        put_c<NSP, CL>(x, y);
+        sfor<0, Net::NS>([&](auto qc) {
+            constexpr int q = decltype(qc)::value;
+            c[q] = ((lds_cdouble*)x.c)[q];
+        });
+    } else {
+        const double v = (CL && PCK_GRP_CLAMP) ? fmax(y, 0.0) : y;
+        sfor<0, Net::NS>([&](auto qc) {
+            constexpr int q = decltype(qc)::value;
+            c[q] = Net::dyn(q, 0) * gbcast_k<G>(v, q);
+        });
+    }
 }
 
 // S(gl, j): the calling lane's coefficient of column J (0 off its row).  gl

@@ -5,9 +5,10 @@ networks: hipcc --offload-arch=gfx950 on this container, reporting each
 kernel's VGPRs, spills, occupancy and code size from the compiler's
 resource-usage remarks.  No GPU needed.
 
-    python tools/ct_compile_check.py [ch4|dmtm|synthetic ...] [--tables]
+    python tools/ct_compile_check.py [ch4|dmtm|synthetic ...] [--tables] [-DNAME=VALUE ...]
 
---tables builds the record-table kernel of the same exact size instead.
+--tables builds the record-table kernel of the same exact size instead;
+-D options go to hipcc (e.g. -DPCK_GRP_WAVES16=3, -DPCK_CT_CHUNK=2).
 """
 import os
 import re
@@ -42,14 +43,15 @@ def main():
     from gen_networks import emit
     global TABLES
     TABLES = '--tables' in sys.argv
-    names = [a for a in sys.argv[1:] if not a.startswith('--')] or ['dmtm', 'ch4', 'synthetic']
+    defs = [a for a in sys.argv[1:] if a.startswith('-D')]
+    names = [a for a in sys.argv[1:] if not a.startswith('-')] or ['dmtm', 'ch4', 'synthetic']
     for name in names:
         plan = plan_of(name)
         NS = len(plan.dyn)
         G = 16 if NS <= 16 else 32 if NS <= 32 else 64
-        src = ('#define PCK_GRP_EXACT 1\n#define PCK_GRP_BAL 0\n#include "mk_solver.h"\nnamespace pck {\nnamespace nets {\n'
+        src = ('#define PCK_GRP_EXACT 1\n#ifndef PCK_CHK_P\n#define PCK_CHK_P 1\n#endif\n#define PCK_GRP_BAL 0\n#include "mk_solver.h"\nnamespace pck {\nnamespace nets {\n'
                + emit('Jit', plan) + '\n}\n}\n#include "mk_group.h"\n'
-               'template __global__ void pck::k_solve_grp<%d, %d, 1, false, false, %s>('
+               'template __global__ void pck::k_solve_grp<%d, %d, PCK_CHK_P, false, false, %s>('
                'pck::NetView, pck::GrpView, pck::CondView, const double*, const double*, int64_t, pck::SolveArgs, '
                'pck::GrpArgs);\n' % (NS, G, 'pck::NoNet' if TABLES else 'pck::nets::Jit'))
         with tempfile.TemporaryDirectory() as d:
@@ -58,7 +60,7 @@ def main():
             cmd = ['/opt/rocm/bin/hipcc', '--offload-arch=gfx950', '-O3', '-std=c++17', '-fno-signed-zeros',
                    '--cuda-device-only', '-c', '-I' + os.path.join(ROOT, 'include'),
                    '-I' + os.path.join(ROOT, 'pycatkin_amd', 'csrc'), '-Rpass-analysis=kernel-resource-usage',
-                   '-o', os.path.join(d, 'k.o'), f]
+                   *defs, '-o', os.path.join(d, 'k.o'), f]
             p = subprocess.run(cmd, capture_output=True, text=True)
             if p.returncode:
                 print(name, 'FAILED'); print(p.stderr[-4000:]); continue
