@@ -1144,7 +1144,7 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
         if constexpr (TRAJ) {
             using namespace rodas4_dense;
             d2 = D21 * k1 + D22 * k2 + D23 * k3 + D24 * k4 + D25 * k5;
-            d3 = D31 * k1 + D32 * k2 + D33 * k3 + D34 * k4 + D35 * k5;
+            d3 = D3_K5_ONLY ? D35 * k5 : D31 * k1 + D32 * k2 + D33 * k3 + D34 * k4 + D35 * k5;
         }
         u += k6;
         const double sc = atol + rtol * fmax(fabs(y), fabs(u));
@@ -1336,6 +1336,7 @@ __device__ __forceinline__ int grp_newton(const NetView& nv, const GrpView& gv, 
         if (!(fin > 0.0)) break;
         const double zmax = gmax<G>(x.row ? fabs(z) : 0.0);
         const double rel = gmax<G>(x.row ? fabs(dz) / fmax(fabs(z), 1e-12 * zmax + 1e-300) : 0.0);
+        if (prev < PCK_STEP_FLOOR && rel > prev) { z = z_prev; conv = true; break; }   // mk_solver.h: the step floor
         if (rel < 1e-12 || (it >= 2 && rel < 1e-7 && rel > 0.5 * prev)) { conv = true; break; }
         lastq = rel / prev;
         linear = (rel > 0.25 * prev) ? linear + 1 : 0;

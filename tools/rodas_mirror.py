@@ -1,9 +1,10 @@
 """Diagnostic (test infrastructure, never the product): a numpy restatement of
-the device Rodas4 integrator of csrc/mk_solver.h / mk_group.h (same stages,
+the device Rosenbrock integrator (RODAS4P; METHOD=rodas4 for RODAS4) of csrc/mk_solver.h / mk_group.h (same stages,
 initial step, error norm, step controller and site-balance projection) that
 records the step history of one condition of the oracle's models.
 
     python tools/rodas_mirror.py synthetic IDX     (a condition of the synthetic bench config)
+    python tools/rodas_mirror.py volcano ECO EO    (a volcano grid point, steady-rule tolerances)
 """
 import json
 import os
@@ -24,11 +25,25 @@ Cc = [[], [-5.6688], [-2.430093356833875, -0.2063599157091915],
       [7.496443313967647, -10.24680431464352, -33.99990352819905, 11.70890893206160],
       [8.083246795921522, -7.981132988064893, -31.52159432874371, 16.31930543123136, -6.058818238834054]]
 
-
 DD2 = [10.12623508344586, -7.487995877610167, -34.80091861555747, -7.992771707568823, 1.025137723295662]
 DD3 = [-0.6762803392801253, 6.087714651680015, 16.43084320892478, 24.76722511418386, -6.594389125716872]
 
+# the device default (csrc/mk_solver.h PCK_RODAS4P=1): Steinebach's RODAS4P
+# and its stiff-limit dense output; METHOD=rodas4 keeps the Hairer-Wanner set
+# above (the device's PCK_RODAS4P=0)
+if os.environ.get('METHOD', 'rodas4p') == 'rodas4p':
+    A = [[], [3.0], [1.831036793486759, 0.4955183967433795],
+         [2.304376582692669, -0.05249275245743001, -1.176798761832782],
+         [-7.170454962423024, -4.741636671481785, -16.31002631330971, -1.062004044111401]]
+    Cc = [[], [-12.0], [-8.791795173947035, -2.207865586973518],
+          [10.81793056857153, 6.780270611428266, 19.53485944642410],
+          [34.19095006749676, 15.49671153725963, 54.74760875964130, 14.16005392148534],
+          [34.62605830930532, 15.30084976114473, 56.99955578662667, 18.40807009793095, -5.714285714285717]]
+    DD2 = [26.549127843114945, 10.967258456569217, 35.997973167097996, 8.496032352891316, -40.0 / 7.0]
+    DD3 = [0.0, 0.0, 0.0, 0.0, 32.0 / 7.0]
+
 PIVLOG = []
+COMP = []       # COMP=1: (t, y, per-species squared scaled error) of every step
 
 
 def gpu_lu_solve(W, rhs_list):
@@ -139,6 +154,8 @@ def rodas4(f, J, y, t0, t_end, rtol, atol, cons=None, max_steps=200000, cons_row
         fin = np.all(np.isfinite(unew))
         scl = atol + rtol * np.maximum(np.abs(y), np.abs(unew))
         q = np.mean((ks[5] / scl) ** 2) if fin else np.inf
+        if os.environ.get('COMP'):
+            COMP.append((t, y.copy(), (ks[5] / scl) ** 2))
         fac = 0.9 * q ** -0.125 if q > 0 else np.inf
         neg = (unew < -atol) & (os.environ.get('NOPOS') is None)
         pf = float(np.min((y[neg] + atol) / (y[neg] - unew[neg]))) if np.any(neg) else 1.0
@@ -215,9 +232,25 @@ def dmtm_model(T):
     return O.ClassicModel(spec, T=T, p=float(os.environ.get('P', spec['system']['p']))), [T]
 
 
+def volcano_model(eco, eo):
+    import copy
+    from oracle import mk_oracle as O
+    spec = O.load_spec(os.path.join(ROOT, 'tests', 'golden', 'inputs', 'COOxVolcano', 'input.json'))
+    spec = copy.deepcopy(spec)
+    O.set_volcano_point(spec, eco, eo, None)
+    return O.ClassicModel(spec, T=None), [eco, eo]
+
+
 def main():
     which = sys.argv[1]
-    if which == 'dmtm':
+    if which == 'volcano':
+        m, D = volcano_model(float(sys.argv[2]), float(sys.argv[3]))
+        D = np.array(D)
+        idx = 0
+        sys.argv = sys.argv[:2] + sys.argv[4:]
+        # pycatkin_amd/classes/system.py STEADY_TRANSIENT, the input's t_end
+        t_end, rtol, atol = 3600.0, float(os.environ.get('RTOL', 1e-6)), float(os.environ.get('ATOL', 1e-22))
+    elif which == 'dmtm':
         m, D = dmtm_model(float(sys.argv[2]))
         D = np.array(D)
         idx = 0
