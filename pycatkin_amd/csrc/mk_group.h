@@ -1000,6 +1000,10 @@ __device__ __forceinline__ double grp_solve(const Grp<NSP>& x, const LU<NSP>& F,
 // RODAS4 on the group (same scheme, controller, projection and positivity
 // rule as mk_solver.h: integrate)
 // ---------------------------------------------------------------------------
+// removal of the stage increments' conserved-total drift along y (see grp_integrate)
+#ifndef PCK_GRP_KPROJ
+#define PCK_GRP_KPROJ 1
+#endif
 template <int NSP, int G, int P, bool TRAJ = false, class Net = NoNet>
 __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& gv, const Grp<NSP>& x, double& y,
                                              double t0, double t_end, double rtol, double atol, int max_steps,
@@ -1034,6 +1038,25 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
             cpos[l] = gmin<G>(ci[l]) >= 0.0;
         }
     }
+    // stage increments keep the conserved totals (PCK_GRP_KPROJ): C k = 0
+    // holds exactly for the ODE (C f = 0, C J = 0), but in floating point
+    // C f is the rounding of the species balances, ~eps x the gross fluxes
+    // (1e11 / s on DMTM), and the stage solve multiplies it by h g along the
+    // Jacobian's null direction -- at h ~ 1e9 s on a steady state that drift
+    // swamps the tolerance and the step is rejected over and over.  The
+    // drift is removed along y (the direction of the multiplicative
+    // projection after the step, so a species' correction scales with its
+    // size); an orthogonal projection spreads the large species' rounding
+    // onto the tiny ones and stalls the solve (tools/rodas_mirror.py KPROJ).
+    double icy[PCK_MAX_CONS];
+    auto kproj = [&](double k) {
+        if (PCK_GRP_KPROJ && !crows) {
+#pragma unroll
+            for (int l = 0; l < PCK_MAX_CONS; ++l)
+                if (l < nv.NCONS && cpos[l]) k -= gsum<G>(ci[l] * k) * icy[l] * y;
+        }
+        return k;
+    };
     double h;
     {
         const double sc = atol + rtol * fabs(y);
@@ -1094,12 +1117,21 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
             if (!(h > 2.220446049250313e-15 * fmax(fabs(t), 1e-300))) return PCK_ST_STEPFAIL;
             continue;
         }
+        if (PCK_GRP_KPROJ && !crows) {
+#pragma unroll
+            for (int l = 0; l < PCK_MAX_CONS; ++l) {
+                if (l < nv.NCONS && cpos[l]) {
+                    const double cy = gsum<G>(ci[l] * y);
+                    icy[l] = (cy > 0.0) ? 1.0 / cy : 0.0;
+                }
+            }
+        }
         double k1, k2, k3, k4, k5, k6, fu, u;
         if constexpr (IsCt<Net>::v) {
             // the straight-line network code is large: one rhs and one solve
             // site for the five stages (the same stage formulas, unused
             // coefficients zero; u_6 = u_5 + k5 as a sixth row)
-            PCK_PH(2, (k1 = grp_solve<NSP, G>(x, F, keep * F0)));
+            PCK_PH(2, (k1 = kproj(grp_solve<NSP, G>(x, F, keep * F0))));
             k2 = k3 = k4 = k5 = k6 = 0.0;
 #pragma unroll 1
             for (int st = 2; st <= 6; ++st) {
@@ -1116,8 +1148,8 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
                 u = y + b1 * k1 + b2 * k2 + b3 * k3 + b4 * k4 + b5 * k5;
                 PCK_PH(3, (fu = grp_rhs<NSP, G, CLAMP, Net>(gv, x, u)));
                 double kn;
-                PCK_PH(2, (kn = grp_solve<NSP, G>(x, F, keep * (fu + ih * (e1 * k1 + e2 * k2 + e3 * k3 + e4 * k4 +
-                                                                           e5 * k5)))));
+                PCK_PH(2, (kn = kproj(grp_solve<NSP, G>(x, F, keep * (fu + ih * (e1 * k1 + e2 * k2 + e3 * k3 +
+                                                                                 e4 * k4 + e5 * k5))))));
                 k2 = (st == 2) ? kn : k2;
                 k3 = (st == 3) ? kn : k3;
                 k4 = (st == 4) ? kn : k4;
@@ -1125,20 +1157,21 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
                 k6 = (st == 6) ? kn : k6;
             }
         } else {
-        PCK_PH(2, (k1 = grp_solve<NSP, G>(x, F, keep * F0)));
+        PCK_PH(2, (k1 = kproj(grp_solve<NSP, G>(x, F, keep * F0))));
         PCK_PH(3, (fu = grp_rhs<NSP, G, CLAMP, Net>(gv, x, y + a21 * k1)));
-        PCK_PH(2, (k2 = grp_solve<NSP, G>(x, F, keep * (fu + ih * (C21 * k1)))));
+        PCK_PH(2, (k2 = kproj(grp_solve<NSP, G>(x, F, keep * (fu + ih * (C21 * k1))))));
         PCK_PH(3, (fu = grp_rhs<NSP, G, CLAMP, Net>(gv, x, y + a31 * k1 + a32 * k2)));
-        PCK_PH(2, (k3 = grp_solve<NSP, G>(x, F, keep * (fu + ih * (C31 * k1 + C32 * k2)))));
+        PCK_PH(2, (k3 = kproj(grp_solve<NSP, G>(x, F, keep * (fu + ih * (C31 * k1 + C32 * k2))))));
         PCK_PH(3, (fu = grp_rhs<NSP, G, CLAMP, Net>(gv, x, y + a41 * k1 + a42 * k2 + a43 * k3)));
-        PCK_PH(2, (k4 = grp_solve<NSP, G>(x, F, keep * (fu + ih * (C41 * k1 + C42 * k2 + C43 * k3)))));
+        PCK_PH(2, (k4 = kproj(grp_solve<NSP, G>(x, F, keep * (fu + ih * (C41 * k1 + C42 * k2 + C43 * k3))))));
         u = y + a51 * k1 + a52 * k2 + a53 * k3 + a54 * k4;
         PCK_PH(3, (fu = grp_rhs<NSP, G, CLAMP, Net>(gv, x, u)));
-        PCK_PH(2, (k5 = grp_solve<NSP, G>(x, F, keep * (fu + ih * (C51 * k1 + C52 * k2 + C53 * k3 + C54 * k4)))));
+        PCK_PH(2, (k5 = kproj(grp_solve<NSP, G>(x, F, keep * (fu + ih * (C51 * k1 + C52 * k2 + C53 * k3 +
+                                                                          C54 * k4))))));
         u += k5;
         PCK_PH(3, (fu = grp_rhs<NSP, G, CLAMP, Net>(gv, x, u)));
-        PCK_PH(2, (k6 = grp_solve<NSP, G>(x, F, keep * (fu + ih * (C61 * k1 + C62 * k2 + C63 * k3 + C64 * k4 +
-                                                                     C65 * k5)))));
+        PCK_PH(2, (k6 = kproj(grp_solve<NSP, G>(x, F, keep * (fu + ih * (C61 * k1 + C62 * k2 + C63 * k3 +
+                                                                          C64 * k4 + C65 * k5))))));
         }
         double d2 = 0.0, d3 = 0.0;                 // dense output (mk_solver.h: rodas4_dense)
         if constexpr (TRAJ) {

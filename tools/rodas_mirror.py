@@ -140,6 +140,17 @@ def rodas4(f, J, y, t0, t_end, rtol, atol, cons=None, max_steps=200000, cons_row
             except np.linalg.LinAlgError:
                 ok = False
                 break
+            if os.environ.get('KPROJ') and cons is not None:
+                # KPROJ=1: the conserved totals' drift removed along y (the
+                # multiplicative projection's direction); KPROJ=orth:
+                # orthogonally (spreads rounding onto tiny species: A/B only)
+                if os.environ['KPROJ'] == 'orth':
+                    for crow in np.linalg.qr(np.asarray(cons, float).T)[0].T:
+                        k = k - (crow @ k) * crow
+                else:
+                    for crow in np.asarray(cons, float):
+                        if np.all(crow >= 0.0) and crow @ y > 0.0:
+                            k = k - y * ((crow @ k) / (crow @ y))
             ks.append(k)
             if i < 4:
                 u = y + sum(A[i + 1][j] * ks[j] for j in range(i + 1))
