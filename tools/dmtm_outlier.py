@@ -1,3 +1,7 @@
+"""Diagnostic (GPU): the DMTM DRC bench grid's slowest condition (index 2297,
+T 622.22 K, p 644 947 Pa) and two neighbours as plain solves at the input
+tolerances; with a PCK_TRACE build (PCK_LIB=...) the step trace of the first
+into gpurun_out/r4v_trace.npy.  Run per variant: PCK_GRP_CT=0, PCK_JIT=0."""
 import ctypes as C, os, sys, numpy as np
 sys.path.insert(0, '/root/repo')
 import pycatkin_amd as P
