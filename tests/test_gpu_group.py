@@ -439,6 +439,30 @@ def test_dmtm_pressure_sweep_vs_oracle(P, inputs):
         assert np.abs(final[0] - final[2]).max() > 1e-6
 
 
+def test_dmtm_steady_state_at_large_steps_does_not_stall(P, inputs):
+    """The DMTM DRC bench grid's slowest condition (622.2 K, 6.45e5 Pa; gross
+    fluxes ~1e11 /s): on its steady state the rounding of the site balance,
+    multiplied by h g at h ~ 1e9 s, used to drift the stage increments' site
+    total and reject step after step (7 532 steps instead of 176; mk_group.h
+    PCK_GRP_KPROJ, DESIGN.md "Integrator").  The plain solve and its 23-solve
+    DRC take the ordinary step counts and the state matches the oracle's."""
+    s = _dmtm(P, inputs)
+    T = np.full(3, np.linspace(400.0, 800.0, 64)[35])    # bench.py dmtm_drc grid, condition 2297
+    p = np.logspace(4.0, 6.0, 64)[[57, 56, 58]]
+    r = s.solve_batch(T=T, p=p, tof_terms=('r5', 'r9'))
+    assert np.all(r['status'] == 0), r['status']
+    assert r['nsteps'].max() < 400, r['nsteps']
+    d = s.drc_batch(('r5', 'r9'), T=T, p=p, eps=5.0e-2)
+    assert np.all(d['status'] == 0) and d['nsteps'].max() < 23 * 400, d['nsteps']
+    spec = O.load_spec(os.path.join(inputs, 'DMTM', 'input.json'))
+    m = O.ClassicModel(spec, T=float(T[0]), p=float(p[0]))
+    yT, _ = m.solve_odes(rtol=1e-10, atol=1e-14)
+    plan = s.plan(('r5', 'r9'))
+    ref = np.array([yT[m.idx[n]] for n in plan.dyn])
+    # the transient at the input tolerances (1e-6 / 1e-8) against a tight one
+    assert np.all(np.abs(r['y'][:, 0] - ref) <= 1e-4 * np.abs(ref) + 1e-8), (r['y'][:, 0], ref)
+
+
 def _six_species_net():
     """A 12-species network whose reaction R0 has 6 dynamic participants and
     6 stoichiometric entries (the widest record of the lane-group plan)."""
