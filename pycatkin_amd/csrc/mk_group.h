@@ -1237,7 +1237,7 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
                 if (negf) y = 0.0;
                 PCK_PH(3, (F0 = grp_rhs<NSP, G, CLAMP, Net>(gv, x, y)));
             }
-            h *= fmin(6.0, fmax(0.2, fac));
+            h *= fmin(PCK_FACMAX, fmax(0.2, fac));
         } else if (q <= 1.0) {
             h *= fmax(0.1, 0.9 * pf);
         } else {

@@ -1030,7 +1030,15 @@ static int launch_solve(const pck_network* net, const pck_conditions* cond, cons
                            n, W, list, cnt);
         HIPCHK(hipGetLastError());
         SolveArgs pv = a;
-        pv.rtol = fmax(a.rtol, 1e-3);
+        // the preview's rtol floor: 1e-2 (the preview is latency-bound on its
+        // slowest sample: ~80 steps there against ~120 at 1e-3; the volcano
+        // step 5.71 -> 5.65 ms with the coarser order, profiles/r4/ab_preview_*);
+        // PCK_PREVIEW_RTOL overrides it (A/B)
+        pv.rtol = fmax(a.rtol, 1e-2);
+        {
+            const char* e = getenv("PCK_PREVIEW_RTOL");
+            if (e) pv.rtol = fmax(a.rtol, atof(e));
+        }
         pv.atol = a.atol * (pv.rtol / a.rtol);       // the same atol / rtol ratio
         {
             // A/B: PCK_PREVIEW_ATOL = a floor of the preview's atol, relative to its rtol

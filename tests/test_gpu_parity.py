@@ -359,10 +359,13 @@ def test_jit_plan_matches_runtime_plan(P, inputs):
     both = (a['status'] == 0) & (b['status'] == 0)
     assert np.mean(both) > 0.9, (np.unique(a['status'], return_counts=True), np.unique(b['status'], return_counts=True))
     assert np.mean(a['status'] != b['status']) < 0.05
-    assert close_cov(a['y'][:, both], b['y'][:, both], rtol=1e-7, floor=1e-14), np.abs(a['y'] - b['y'])[:, both].max()
-    # TOF at north_star's 1e-6: the two compilations round differently, and a
-    # root met at Newton's linear exit (rel < 1e-7) carries that into a tiny
-    # TOF (one of these 463 regular roots: 2.3e-20, 3.1e-7 apart)
+    # coverages and TOF at north_star's 1e-6: the two compilations round
+    # differently, and a root met at Newton's linear exit (rel < 1e-7) or at
+    # its step floor carries that (one of these 463 regular roots: TOF
+    # 2.3e-20, 3.1e-7 apart; a 1e-2 coverage 3.1e-9 apart after PCK_FACMAX 10
+    # moved the transient ends Newton starts from)
+    ya, yb = a['y'][:, both], b['y'][:, both]
+    assert close_cov(ya, yb, rtol=1e-6, floor=1e-14), np.max(np.abs(ya - yb) / np.maximum(np.abs(yb), 1e-14))
     np.testing.assert_allclose(a['tof'][both], b['tof'][both], rtol=1e-6)
 
 

@@ -208,7 +208,7 @@ def rodas4(f, J, y, t0, t_end, rtol, atol, cons=None, max_steps=200000, cons_row
                 if np.any(neg):
                     y = np.where(neg, 0.0, y)
                     F0 = f(y)
-            m = min(6.0, max(0.2, fac))
+            m = min(float(os.environ.get('FACMAX', 10.0)), max(0.2, fac))
             if ctrl == 'pred':
                 err = max(np.sqrt(q), 1e-300)
                 if hacc is not None:
