@@ -363,10 +363,12 @@ def test_jit_plan_matches_runtime_plan(P, inputs):
     # differently, and a root met at Newton's linear exit (rel < 1e-7) or at
     # its step floor carries that (one of these 463 regular roots: TOF
     # 2.3e-20, 3.1e-7 apart; a 1e-2 coverage 3.1e-9 apart after PCK_FACMAX 10
-    # moved the transient ends Newton starts from)
+    # moved the transient ends Newton starts from).  Each build is within
+    # ~1e-6 of the root, so two builds differ by up to twice that (one TOF of
+    # 472: 1.3e-6 apart)
     ya, yb = a['y'][:, both], b['y'][:, both]
     assert close_cov(ya, yb, rtol=1e-6, floor=1e-14), np.max(np.abs(ya - yb) / np.maximum(np.abs(yb), 1e-14))
-    np.testing.assert_allclose(a['tof'][both], b['tof'][both], rtol=1e-6)
+    np.testing.assert_allclose(a['tof'][both], b['tof'][both], rtol=2e-6)
 
 
 def test_jit_can_be_disabled(P, inputs, monkeypatch):
