@@ -2,7 +2,7 @@
 (BASELINE.json configs[2]) and, with --config, the other BASELINE configs.
 
 One step = one batched solve of this rank's share of the workload: kernel (1)
-rate constants from the descriptor energies, kernel (3) Rodas4 transient to
+rate constants from the descriptor energies, kernel (3) RODAS4P transient to
 t_end + Newton steady-state polish, kernel (4) TOF / activity.  Inputs are
 resident in HBM before the timed region.
 
@@ -47,10 +47,10 @@ METRIC = 'steady-state MK solves/sec (whole node) on COOx volcano grid at 1/2/4/
 
 
 # ----------------------------------------------------------------------------
-# algorithmic FLOPs of one Rodas4 step (structural nonzeros only)
+# algorithmic FLOPs of one RODAS4P step (structural nonzeros only)
 # ----------------------------------------------------------------------------
 def flops_per_step(plan):
-    """fp64 FLOPs of one accepted Rodas4 step of kernel (3) on this plan,
+    """fp64 FLOPs of one accepted RODAS4P step of kernel (3) on this plan,
     counting only structurally non-zero work (mk_solver.h: integrate / rhs /
     jac, mk_group.h for the lane-group path): 6 rate evaluations (5 stages +
     F0 at the accepted state), 1 Jacobian, 1 dense LU, 6 triangular solves,
@@ -720,7 +720,7 @@ def main(argv=None):
                     'traffic_source': traffic_src, 'algorithmic_bytes': wl.algo_bytes,
                     'kernel': wl.kernel_name, 'kernel_ms': k3_ms, 'rate_constants_ms': k1_ms,
                     'flops_per_launch': fl, 'flops_structural': fl_struct, 'flops_pmc_f64': fl_pmc,
-                    'flops_per_step': fps, 'flop_count': 'min(structural nonzeros of one accepted Rodas4 step x '
+                    'flops_per_step': fps, 'flop_count': 'min(structural nonzeros of one accepted RODAS4P step x '
                     'integrator steps of rank 0 (first pass + retry; the preview, Newton polish, kernel 1 and TOF not counted), '
                     '64 x (ADD+MUL+TRANS) + 128 x FMA fp64 wave instructions of the committed PMC profile of this '
                     'workload, per launch x solver launches per step)',

@@ -5,7 +5,7 @@ System's _fun_ss / _jac_ss (solver.py:17-418).  Here every rate, Jacobian
 and integration is a launch of the HIP library through the C-ABI:
 
   solve_ode       transient of the surface species from the normalised
-                  initial state to tmax (device Rodas4, the reference's
+                  initial state to tmax (device RODAS4P, the reference's
                   solve_ivp with rtol 1e-10 / atol 1e-12 -- the tolerances
                   solver.py:406-407 hard-codes whatever its arguments say),
                   then test_convergence; solve_ode_batch does it for a batch
@@ -121,7 +121,7 @@ class SteadyStateSolver:
         return self.sys.initial_system[len(self.sys.gas_indices):]
 
     def solve_ode(self, method='RK45', use_jac=True, rtol=1e-10, atol=1e-12, tmax=1e4, test_convergence_kwargs=None):
-        """solver.py:374-418 (device Rodas4 at rtol 1e-10 / atol 1e-12)."""
+        """solver.py:374-418 (device RODAS4P at rtol 1e-10 / atol 1e-12)."""
         Y, ok = self.solve_ode_batch(T=[self.sys.T], tmax=tmax, test_convergence_kwargs=test_convergence_kwargs)
         return SteadyStateResults(Y[:, 0], bool(ok[0]))
 

@@ -438,7 +438,7 @@ class System:
         """Transient solve to t_end (solve_odes), optionally polished to the
         steady state (find_steady), with TOF or activity per condition; with
         t_out, also the dynamic state at those times ('traj' [n_out, NS, n],
-        Rodas4 dense output).
+        RODAS4P dense output).
 
         steady=True: the transient runs at STEADY_TRANSIENT unless rtol / atol
         are given, and the Newton root of its end state is reported (status
