@@ -185,30 +185,6 @@ __device__ __forceinline__ double bc16(double v, int k) {
     }
 }
 
-// lane K (compile-time after unrolling) of the whole wavefront, in VGPRs:
-// DPP row_newbcast puts lane K % 16 of every row across its row, then the
-// gfx950 permlane swaps copy row K / 16 over the other three (two swaps,
-// both results kept, one picked by the compile-time row).  Three dependent
-// VALU steps per 32-bit half, no SGPR round trip (tools/hip/permlane_check.hip
-// checks all 64 x 64 cases on the GPU).
-__device__ __forceinline__ int wbc64i(int v, int k) {
-    int t = 0;
-    switch (k & 15) {
-#define PCK_BC(K) case K: t = __builtin_amdgcn_update_dpp(0, v, 0x150 + K, 0xf, 0xf, false); break;
-        PCK_BC(0) PCK_BC(1) PCK_BC(2) PCK_BC(3) PCK_BC(4) PCK_BC(5) PCK_BC(6) PCK_BC(7)
-        PCK_BC(8) PCK_BC(9) PCK_BC(10) PCK_BC(11) PCK_BC(12) PCK_BC(13) PCK_BC(14) PCK_BC(15)
-#undef PCK_BC
-    }
-    const int r = k >> 4;
-    const auto s32 = __builtin_amdgcn_permlane32_swap(t, t, false, false);
-    const int u = (r < 2) ? (int)s32[0] : (int)s32[1];
-    const auto s16 = __builtin_amdgcn_permlane16_swap(u, u, false, false);
-    return (r & 1) ? (int)s16[1] : (int)s16[0];
-}
-__device__ __forceinline__ double wbc64(double v, int k) {
-    return __hiloint2double(wbc64i(__double2hiint(v), k), wbc64i(__double2loint(v), k));
-}
-
 // broadcast lane `src` (group-uniform) of the group
 template <int G>
 __device__ __forceinline__ double gbcast(double v, int src) {
@@ -934,58 +910,6 @@ __device__ __forceinline__ double grp_solve16(const Grp<NSP>& x, const LU<NSP>& 
     return x.row ? b : 0.0;
 }
 
-// 64-lane groups, rows put in pivot order after the factorisation
-// (PCK_GRP_PERM64): one ds_permute per row entry moves row i to lane
-// step(i), so lane k holds the pivot row of column k.  Both substitutions
-// then broadcast from the constant lane k (v_readlane with an inline lane
-// index) instead of extracting the pivot lane of column k from the packed
-// permutation and moving it through readfirstlane on each of the solve's
-// 100 dependent links.
-#ifndef PCK_GRP_PERM64
-#define PCK_GRP_PERM64 0
-#endif
-#ifndef PCK_GRP_WBC64
-#define PCK_GRP_WBC64 1
-#endif
-template <int NSP>
-__device__ __forceinline__ void grp_pivot_order64(const Grp<NSP>& x, LU<NSP>& F) {
-    const int dst = 4 * ((x.row && F.step < NSP) ? F.step : x.gl);
-#pragma unroll
-    for (int j = 0; j < NSP; ++j) {
-        const int lo = __builtin_amdgcn_ds_permute(dst, __double2loint(F.W[j]));
-        const int hi = __builtin_amdgcn_ds_permute(dst, __double2hiint(F.W[j]));
-        F.W[j] = __hiloint2double(hi, lo);
-    }
-    F.src = __builtin_amdgcn_ds_permute(dst, x.gl);
-}
-
-template <int NSP>
-__device__ __forceinline__ double grp_solve64(const Grp<NSP>& x, const LU<NSP>& F, double b) {
-    {                                               // b into pivot order
-        const int a = 4 * F.src;
-        const int lo = __builtin_amdgcn_ds_bpermute(a, __double2loint(b));
-        const int hi = __builtin_amdgcn_ds_bpermute(a, __double2hiint(b));
-        b = __hiloint2double(hi, lo);
-    }
-#pragma unroll
-    for (int k = 0; k < NSP; ++k) {
-        if (k < x.NS) {
-            const double bk = PCK_GRP_WBC64 ? wbc64(b, k) : rlane(b, k);
-            if (x.gl > k) b = fma(-F.W[k], bk, b);
-        }
-    }
-#pragma unroll
-    for (int kk = 0; kk < NSP; ++kk) {
-        const int k = NSP - 1 - kk;
-        if (k < x.NS) {
-            const double xk = PCK_GRP_WBC64 ? wbc64(b * F.W[k], k) : rlane(b * F.W[k], k);
-            if (x.gl < k) b = fma(-F.W[k], xk, b);
-            if (x.gl == k) b = xk;
-        }
-    }
-    return x.row ? b : 0.0;
-}
-
 #ifndef PCK_GRP_READLANE
 #define PCK_GRP_READLANE 1
 #endif
@@ -1045,7 +969,6 @@ __device__ __forceinline__ bool grp_lu(const Grp<NSP>& x, LU<NSP>& F) {
             F.pk.set(k, p);
         }
     }
-    if constexpr (G == 64 && PCK_GRP_PERM64) grp_pivot_order64<NSP>(x, F);
     return ok;
 }
 
@@ -1053,7 +976,6 @@ __device__ __forceinline__ bool grp_lu(const Grp<NSP>& x, LU<NSP>& F) {
 template <int NSP, int G>
 __device__ __forceinline__ double grp_solve(const Grp<NSP>& x, const LU<NSP>& F, double b) {
     if constexpr (G == 16 && NSP <= 16) return grp_solve16<NSP>(x, F, b);
-    if constexpr (G == 64 && PCK_GRP_PERM64) return grp_solve64<NSP>(x, F, b);
 #pragma unroll
     for (int k = 0; k < NSP; ++k) {
         if (k < x.NS) {
