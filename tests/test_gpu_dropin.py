@@ -146,6 +146,29 @@ def test_volcano_fixture_parity(P, inputs):
         assert f['max_rel_cov'] <= 2.0 * ROOT_DIST + RTOL, f
 
 
+def test_newton_step_floor_node(P, inputs):
+    """Fixture node 2502 (E_CO -0.606, E_O -2.040: sO 0.99996, sO2 3.6e-5)
+    is a reached steady state (the oracle's criterion 1.9e-13), but Newton's
+    second step from the transient end is rounding amplified ~1e6 by the
+    Jacobian.  The step floor (mk_solver.h: PCK_STEP_FLOOR) returns the
+    iterate before that step: status 0 and the oracle's root at 1e-9, where
+    the iteration used to wander to its linear-convergence exit (status 4)."""
+    from pycatkin_amd.functions.volcano import set_volcano_energies
+    fx = dict(np.load(os.path.join(GOLDEN, 'volcano_fixture.npz')))
+    lo, hi, G = fx['grid']
+    be = np.linspace(lo, hi, int(G))
+    k = 2502
+    assert fx['regular'][k] and fx['crit'][k] < 1e-12
+    s = P.read_from_input_file(os.path.join(inputs, 'COOxVolcano', 'input.json'))
+    set_volcano_energies(s)
+    r = s.solve_batch(T=np.full(1, 600.0), desc={'ECO': be[fx['i'][k:k + 1]], 'EO': be[fx['j'][k:k + 1]]},
+                      tof_terms=('CO_ox',), steady=True)
+    assert r['status'][0] == 0, r['status']
+    plan = s.plan(('CO_ox',))
+    y = r['y'][[plan.dyn.index(str(n)) for n in fx['dyn']], 0]
+    np.testing.assert_allclose(y, fx['y_root'][k], rtol=1e-9, atol=1e-20)
+
+
 def test_degenerate_points_through_drop_in_api(P, inputs):
     """System.find_steady() / activity(ss_solve=True) on a degenerate root
     (status 4) return -- as the reference's least_squares path returns -- the
