@@ -761,33 +761,50 @@ __global__ void __launch_bounds__(256) k_preview_list(int64_t n, int64_t W, int6
     if (i == 0) *cnt = (int32_t)(W * PCK_PREVIEW_LANES);
 }
 
-// descending counting sort of the wavefronts by their preview key (one block).
-// (A grid-wide histogram / scan / scatter took 0.17 ms against this block's
-// 0.07 ms -- its global atomics contend on a few hundred bins -- and its
-// order inside a bin cost the first pass 0.15 ms more: profiles/r3/wave_sort_ab.)
-__global__ void __launch_bounds__(1024) k_wave_order(int64_t n, int64_t W, const int32_t* ns, int32_t* order) {
+// (A grid-wide histogram / scan / scatter sort took 0.17 ms against the one-
+// block sort's 0.07 ms -- its global atomics contend on a few hundred bins --
+// and its order inside a bin cost the first pass 0.15 ms more:
+// profiles/r3/wave_sort_ab.)
+// the sort key of every wavefront (the max preview step count of its samples),
+// gathered from the scattered preview outputs by the whole grid, so that the
+// one-block sort below reads W contiguous keys (it read 4 W scattered lines
+// itself: ~28 of its 70 us)
+__global__ void __launch_bounds__(256) k_wave_keys(int64_t n, int64_t W, const int32_t* ns, int32_t* wkey) {
+    const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= W) return;
+    int k = 0;
+#pragma unroll
+    for (int l = 0; l < PCK_PREVIEW_LANES; ++l) {
+        int64_t c = w * PCK_SOLVE_BLOCK + preview_lane(l);
+        c = (c < n) ? c : n - 1;
+        k = max(k, ns[c]);
+    }
+    wkey[w] = min(max(k, 0), 1023);
+}
+
+// descending counting sort of the wavefronts by their key (one block).
+__global__ void __launch_bounds__(1024) k_wave_order(int64_t W, const int32_t* wkey, int32_t* order) {
     __shared__ int hist[1024];
     __shared__ int base[1024];
     const int tid = threadIdx.x;
     hist[tid] = 0;
     __syncthreads();
-    auto key = [&](int64_t w) {
-        int k = 0;
-        for (int l = 0; l < PCK_PREVIEW_LANES; ++l) {
-            int64_t c = w * PCK_SOLVE_BLOCK + preview_lane(l);
-            c = (c < n) ? c : n - 1;
-            k = max(k, ns[c]);
-        }
-        return min(max(k, 0), 1023);
-    };
-    for (int64_t w = tid; w < W; w += 1024) atomicAdd(&hist[key(w)], 1);
+    for (int64_t w = tid; w < W; w += 1024) atomicAdd(&hist[wkey[w]], 1);
     __syncthreads();
-    if (tid == 0) {
-        int sum = 0;
-        for (int k = 1023; k >= 0; --k) { base[k] = sum; sum += hist[k]; }
+    // exclusive scan over the bins, descending (heaviest first): Hillis-Steele
+    // on the reversed histogram, one bin per thread
+    const int v = hist[1023 - tid];
+    base[tid] = v;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {
+        const int add = (tid >= off) ? base[tid - off] : 0;
+        __syncthreads();
+        base[tid] += add;
+        __syncthreads();
     }
+    hist[1023 - tid] = base[tid] - v;           // each bin's start: the wavefronts in heavier bins
     __syncthreads();
-    for (int64_t w = tid; w < W; w += 1024) order[atomicAdd(&base[key(w)], 1)] = (int32_t)w;
+    for (int64_t w = tid; w < W; w += 1024) order[atomicAdd(&hist[wkey[w]], 1)] = (int32_t)w;
 }
 
 // The retry list of the wavefronts at positions [0, nw) of a dispatch order
@@ -1020,12 +1037,13 @@ static int launch_solve(const pck_network* net, const pck_conditions* cond, cons
     if (order) {
         const int64_t W = (n + PCK_SOLVE_BLOCK - 1) / PCK_SOLVE_BLOCK;
         const size_t b_list = sizeof(int64_t) * (size_t)W * PCK_PREVIEW_LANES, b_ns = sizeof(int32_t) * (size_t)n;
-        rc = salloc(oscr, b_list + 64 + b_ns + sizeof(int32_t) * (size_t)W, s);
+        rc = salloc(oscr, b_list + 64 + b_ns + 2 * sizeof(int32_t) * (size_t)W, s);
         if (rc) return rc;
         int64_t* list = oscr.as<int64_t>();
         int32_t* cnt = (int32_t*)((char*)list + b_list);
         int32_t* pns = (int32_t*)((char*)list + b_list + 64);
         int32_t* wo = pns + n;
+        int32_t* wkey = wo + W;                     // per-wavefront sort key, compact
         hipLaunchKernelGGL(k_preview_list, dim3((unsigned)((W * PCK_PREVIEW_LANES + 255) / 256)), dim3(256), 0, s,
                            n, W, list, cnt);
         HIPCHK(hipGetLastError());
@@ -1051,7 +1069,9 @@ static int launch_solve(const pck_network* net, const pck_conditions* cond, cons
         pv.idx = list; pv.nidx = cnt; pv.retry_pass = 0; pv.worder = nullptr;
         rc = run_solver(net, cond, pv, grp, ga, traj, kf, kr, s, W * PCK_PREVIEW_LANES);
         if (rc) return rc;
-        hipLaunchKernelGGL(k_wave_order, dim3(1), dim3(1024), 0, s, n, W, pns, wo);
+        hipLaunchKernelGGL(k_wave_keys, dim3((unsigned)((W + 255) / 256)), dim3(256), 0, s, n, W, pns, wkey);
+        HIPCHK(hipGetLastError());
+        hipLaunchKernelGGL(k_wave_order, dim3(1), dim3(1024), 0, s, W, wkey, wo);
         HIPCHK(hipGetLastError());
         a.worder = wo;
     }
