@@ -9,7 +9,7 @@ mkdir -p "$ROOT/pycatkin_amd/_ab"
 (cd "$ROOT" && python3 -c "import __graft_entry__ as g; g.embed_rtc_sources()")
 while [ $# -ge 2 ]; do
   name=$1; flags=$2; shift 2
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fno-signed-zeros -shared -fPIC $flags -I"$ROOT/include" \
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fno-signed-zeros -mllvm -amdgpu-sched-strategy=max-ilp -shared -fPIC $flags -I"$ROOT/include" \
       -o "$ROOT/pycatkin_amd/_ab/lib_$name.so" "$ROOT/pycatkin_amd/csrc/mk_kernels.hip" -lhiprtc &
 done
 wait
