@@ -550,8 +550,11 @@ def cpu_standin_workload(args, rank, world):
 def build_parser():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=10)
-    ap.add_argument('--warmup', type=int, default=2)
+    # defaults: volcano 20 timed after 10 untimed steps (the clock ramps over
+    # the first few: profiles/r4/volcano trace, the solve launch 6.97 -> 5.68 ms
+    # over 8 steps; 10 untimed steps cost ~60 ms); the other configs 5 after 2
+    ap.add_argument('--steps', type=int, default=None)
+    ap.add_argument('--warmup', type=int, default=None)
     ap.add_argument('--config', choices=sorted(CONFIGS), default='volcano')
     ap.add_argument('--scaling', choices=('strong', 'weak'), default='strong')
     ap.add_argument('--grid', type=int, default=1024)
@@ -599,6 +602,10 @@ def _heartbeat(period=45.0):
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     args = build_parser().parse_args(argv)
+    if args.steps is None:
+        args.steps = 20 if args.config == 'volcano' else 5
+    if args.warmup is None:
+        args.warmup = 10 if args.config == 'volcano' else 2
     _heartbeat()
 
     if 'WORLD_SIZE' not in os.environ and args.gpus > 1:
