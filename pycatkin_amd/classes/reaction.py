@@ -4,14 +4,17 @@ turns them into J/mol (x eVtokJ*1e3) and into rate constants per condition.
 """
 from __future__ import annotations
 
-from ..energy import as_form
+from ..energy import as_form, tkeyed
 
 
 def _lin(x):
     """User energies may be floats, LinearForms (descriptor expressions) or
-    dicts keyed by temperature (reaction.py:228-262)."""
+    dicts keyed by temperature (reaction.py:228-262: ``self.dErxn_user[T]``).
+    A dict becomes a per-condition input filled from each condition's T at
+    solve time (energy.tkeyed; a temperature missing from the dict raises
+    KeyError, as the reference's lookup does)."""
     if isinstance(x, dict):
-        raise NotImplementedError('temperature-keyed user energies: pass a LinearForm in TSYM instead')
+        return tkeyed(x)
     return as_form(x)
 
 

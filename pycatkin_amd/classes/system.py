@@ -14,7 +14,7 @@ from typing import NamedTuple
 import numpy as np
 
 from ..constants.physical_constants import R, bartoPa, eVtokJ, h, kB
-from ..energy import LinearForm
+from ..energy import TKEYED, LinearForm
 from .reaction import Reaction
 from .reactor import InfiniteDilutionReactor, Reactor
 from .state import State
@@ -392,6 +392,8 @@ class System:
         for r in self.reactions.values():
             for a in ('dErxn_user', 'dEa_fwd_user', 'dEa_rev_user', 'dGrxn_user', 'dGa_fwd_user', 'dGa_rev_user'):
                 v = getattr(r, a, None)
+                if isinstance(v, dict):             # temperature-keyed (energy.tkeyed)
+                    v = tuple(sorted((float(k), float(x)) for k, x in v.items()))
                 out.append(repr(v) if isinstance(v, LinearForm) else v)
         return tuple(out)
 
@@ -401,9 +403,17 @@ class System:
         p = self.params['pressure'] if p is None else p
         d = None
         if plan.descriptors:
-            if desc is None:
-                raise ValueError('network depends on descriptors %s' % plan.descriptors)
-            cols = [np.broadcast_to(np.asarray(desc[k], float), (n,)) for k in plan.descriptors]
+            given = [k for k in plan.descriptors if not k.startswith('@T:')]
+            if given and desc is None:
+                raise ValueError('network depends on descriptors %s' % given)
+            Tn = np.broadcast_to(np.asarray(T, float), (n,))
+            cols = []
+            for k in plan.descriptors:
+                if k.startswith('@T:'):             # temperature-keyed user energy (energy.tkeyed)
+                    table = TKEYED[k]
+                    cols.append(np.array([table[float(t)] for t in Tn]))
+                else:
+                    cols.append(np.broadcast_to(np.asarray(desc[k], float), (n,)))
             d = np.stack(cols)
         if fix is None:
             if plan.formulation == 'patched':

@@ -17,7 +17,7 @@ from __future__ import annotations
 import itertools
 import numbers
 
-__all__ = ['LinearForm', 'Descriptor', 'TSYM', 'PSYM', 'clamp0', 'as_form']
+__all__ = ['LinearForm', 'Descriptor', 'TSYM', 'PSYM', 'clamp0', 'as_form', 'tkeyed', 'TKEYED']
 
 _clamp_ids = itertools.count()
 
@@ -121,6 +121,23 @@ def as_form(x):
 def Descriptor(name):
     """A per-condition input (eV), e.g. the CO / O binding energies of a volcano."""
     return LinearForm({('desc', str(name)): 1.0})
+
+
+TKEYED = {}
+"""Temperature-keyed user energies (reaction.py:228-262: ``dErxn_user[T]``):
+descriptor name -> {T: value in eV}.  System._inputs fills such a descriptor's
+column from each condition's temperature."""
+
+
+def tkeyed(values):
+    """A user energy given as a dict keyed by temperature, as a per-condition
+    descriptor named after its content (the same dict is the same descriptor,
+    so a network's structural digest does not depend on object identity)."""
+    table = {float(k): float(v) for k, v in values.items()}
+    import hashlib
+    name = '@T:' + hashlib.sha1(repr(sorted(table.items())).encode()).hexdigest()[:16]
+    TKEYED[name] = table
+    return Descriptor(name)
 
 
 TSYM = LinearForm({('T',): 1.0})

@@ -1,0 +1,59 @@
+"""Temperature-keyed user energies (reference reaction.py:228-262: a user
+energy may be a dict indexed by the condition's temperature)."""
+import os
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+INPUTS = os.path.join(HERE, 'golden', 'inputs')
+TS = [550.0, 575.0, 600.0, 625.0, 650.0]
+VALS = [0.80, 0.84, 0.79, 0.91, 0.86]
+
+
+def _volcano(P, table):
+    from pycatkin_amd.functions.volcano import set_volcano_energies
+    s = P.read_from_input_file(os.path.join(INPUTS, 'COOxVolcano', 'input.json'))
+    set_volcano_energies(s)
+    s.reactions['CO_ox'].dEa_fwd_user = table
+    s._plans.clear()
+    return s
+
+
+def test_tkeyed_energy_is_a_temperature_filled_input():
+    """The dict becomes a per-condition input named after its content; the
+    host fills it from each condition's T (CPU, no device call)."""
+    import pycatkin_amd as P
+    s = _volcano(P, dict(zip(TS, VALS)))
+    plan = s.plan(('CO_ox',))
+    names = [k for k in plan.descriptors if k.startswith('@T:')]
+    assert len(names) == 1 and set(plan.descriptors) == {'ECO', 'EO', names[0]}
+    T = np.array([600.0, 550.0, 650.0, 600.0])
+    _, _, d, _, _, _ = s._inputs(None, plan, T.size, T, None, {'ECO': -1.0, 'EO': -1.0}, None, None, None)
+    col = d[plan.descriptors.index(names[0])]
+    np.testing.assert_array_equal(col, [0.79, 0.80, 0.86, 0.79])
+    # the same table is the same input (structural digest independent of identity)
+    s2 = _volcano(P, {int(t): v for t, v in zip(TS, VALS)})
+    assert [k for k in s2.plan(('CO_ox',)).descriptors if k.startswith('@T:')] == names
+    # a temperature the dict does not hold: KeyError, as the reference's lookup
+    with pytest.raises(KeyError):
+        s._inputs(None, plan, 2, np.array([600.0, 610.0]), None, {'ECO': -1.0, 'EO': -1.0}, None, None, None)
+
+
+@pytest.mark.gpu
+def test_tkeyed_batch_matches_per_temperature_constants():
+    """One batched solve over five temperatures with a T-keyed barrier equals
+    five solves with that barrier as a plain number (steady states and TOF at
+    1e-10; the two networks compile differently, so not bitwise)."""
+    import pycatkin_amd as P
+    desc = {'ECO': -1.2, 'EO': -1.1}
+    s = _volcano(P, dict(zip(TS, VALS)))
+    a = s.solve_batch(T=np.array(TS), desc=desc, tof_terms=('CO_ox',), steady=True)
+    for k, (T, v) in enumerate(zip(TS, VALS)):
+        s1 = _volcano(P, v)
+        b = s1.solve_batch(T=np.array([T]), desc=desc, tof_terms=('CO_ox',), steady=True)
+        assert a['status'][k] == b['status'][0], (T, a['status'][k], b['status'][0])
+        np.testing.assert_allclose(a['y'][:, k], b['y'][:, 0], rtol=1e-10, atol=1e-20)
+        np.testing.assert_allclose(a['tof'][k], b['tof'][0], rtol=1e-10)
+    # the barrier really enters: the TOFs differ across temperatures
+    assert np.unique(np.round(np.log10(np.abs(a['tof'])), 6)).size == len(TS)
