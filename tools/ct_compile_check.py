@@ -5,7 +5,7 @@ networks: hipcc --offload-arch=gfx950 on this container, reporting each
 kernel's VGPRs, spills, occupancy and code size from the compiler's
 resource-usage remarks.  No GPU needed.
 
-    python tools/ct_compile_check.py [ch4|dmtm|synthetic ...] [--tables] [-DNAME=VALUE ...]
+    python tools/ct_compile_check.py [ch4|dmtm|synthetic ...] [--tables] [-DNAME=VALUE ...] [--llvm=OPT ...]
 
 --tables builds the record-table kernel of the same exact size instead;
 -D options go to hipcc (e.g. -DPCK_GRP_WAVES16=3, -DPCK_CT_CHUNK=2).
@@ -44,6 +44,9 @@ def main():
     global TABLES
     TABLES = '--tables' in sys.argv
     defs = [a for a in sys.argv[1:] if a.startswith('-D')]
+    for a in sys.argv[1:]:                  # --llvm=OPT -> -mllvm OPT
+        if a.startswith('--llvm='):
+            defs += ['-mllvm', a[len('--llvm='):]]
     names = [a for a in sys.argv[1:] if not a.startswith('-')] or ['dmtm', 'ch4', 'synthetic']
     for name in names:
         plan = plan_of(name)
