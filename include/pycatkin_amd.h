@@ -191,6 +191,12 @@ typedef struct {
  * size): y and tof are the first pass's transient end at the caller's
  * tolerances -- what the reference's own lsoda path reports */
 #define PCK_ST_NEWTON_LOOSE 5
+/* pck_drc with newton: the 2R+1 solves of a condition fall on both sides of
+ * the steady rule (some report a reached root, PCK_ST_OK, others the
+ * transient end, PCK_ST_NEWTON / _LOOSE): the central differences then mix
+ * two definitions of the answer and xi measures the rule switching, not rate
+ * control.  xi / tof0 are still written. */
+#define PCK_ST_DRC_MIXED 6
 
 int pck_abi_version(void);
 const char* pck_last_error(void);
@@ -257,7 +263,8 @@ int pck_solve(const pck_network* net, const pck_conditions* cond,
  * xi[j][ld_xi] = (TOF(k_j*(1+eps)) - TOF(k_j*(1-eps))) / (2 eps TOF0).
  * tof0 (optional) receives the unperturbed TOF; status (optional) the worst
  * status of the 2R+1 solves (PCK_ST_NONFINITE also for a zero / non-finite
- * TOF0); nsteps (optional) the sum of their integrator steps. */
+ * TOF0; PCK_ST_DRC_MIXED where they mix reached roots and transient ends);
+ * nsteps (optional) the sum of their integrator steps. */
 int pck_drc(const pck_network* net, const pck_conditions* cond,
             const pck_solve_params* prm, double* xi, int64_t ld_xi,
             double* tof0, int32_t* status, int32_t* nsteps, void* stream);

@@ -32,7 +32,7 @@ RX_ARRHENIUS, RX_ADS_KEQ, RX_DES_KEQ, RX_ADS_KDES, RX_DES_KDES = range(5)
 TH_VIB, TH_GAS = 1, 2
 MAX_DYN, MAX_DYN_LANE, MAX_RXN, MAX_CONS, MAX_TOF = 64, 8, 256, 4, 16
 PLAN_AUTO, PLAN_RUNTIME, PLAN_GROUP = 0, 1, 2
-ST_OK, ST_MAXSTEPS, ST_STEPFAIL, ST_NONFINITE, ST_NEWTON, ST_NEWTON_LOOSE = range(6)
+ST_OK, ST_MAXSTEPS, ST_STEPFAIL, ST_NONFINITE, ST_NEWTON, ST_NEWTON_LOOSE, ST_DRC_MIXED = range(7)
 E_ARG, E_HIP, E_SIZE = -1, -2, -3
 
 

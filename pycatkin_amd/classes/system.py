@@ -642,10 +642,10 @@ class System:
         reported) and 5 (the same after a failed `retry` pass: the first
         pass's transient) are results where the reference's steady-state path
         would return one."""
-        if st != 0 and not (degenerate_ok and st in (4, 5)):
+        if st != 0 and not (degenerate_ok and st in (4, 5, 6)):
             raise RuntimeError('%s: device solver status %d (1 max steps, 2 step failure, 3 non-finite, '
                                '4 no steady state reached: transient end, 5 the same with the first-pass '
-                               'transient)' % (what, st))
+                               'transient, 6 a DRC mixing reached roots and transient ends)' % (what, st))
 
     def reaction_terms(self, y):
         """old_system.py:202-225: rates (n_reactions, 2) at the full state y."""
@@ -696,6 +696,11 @@ class System:
         solve_batch's rule (a root reached, or the transient end at t_end)."""
         r = self.drc_batch(tof_terms, T=[self.params['temperature']], eps=eps, steady=ss_solve)
         self._check(r['status'][0], 'degree_of_rate_control', degenerate_ok=True)
+        if r['status'][0] == 6:
+            import warnings
+            warnings.warn('degree_of_rate_control: the perturbed solves fall on both sides of the steady rule '
+                          '(some reached a root, some report the transient end at t_end): the central '
+                          'differences mix the two and xi measures the rule switching (status 6)')
         return {k: float(r[k][0]) for k in self.reactions}
 
     # patched-API steady state (system.py:566-639)

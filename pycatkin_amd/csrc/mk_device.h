@@ -185,6 +185,51 @@ __device__ __forceinline__ double rcp(double x) {
 #endif
 }
 
+// Double-double arithmetic (hi + lo, |lo| <= ulp(hi) / 2) for the Newton
+// refinement's residual (mk_solver.h: newton): error-free products by FMA
+// and Knuth's two-sum, so a balance of 1e11 / s fluxes that cancel to O(1)
+// keeps ~30 digits instead of the ~5 the plain evaluation leaves.
+struct dd {
+    double hi, lo;
+};
+// no FMA contraction in these: the error terms must be computed as written
+// (a contracted a*b feeding its own error term would cancel it)
+#pragma clang fp contract(off)
+__device__ __forceinline__ dd dd_of(double a) { return {a, 0.0}; }
+__device__ __forceinline__ dd two_prod(double a, double b) {
+    const double p = a * b;
+    return {p, __builtin_fma(a, b, -p)};
+}
+__device__ __forceinline__ dd two_sum(double a, double b) {
+    const double s = a + b;
+    const double bb = s - a;
+    return {s, (a - (s - bb)) + (b - bb)};
+}
+__device__ __forceinline__ dd quick_two_sum(double a, double b) {
+    const double s = a + b;
+    return {s, b - (s - a)};
+}
+__device__ __forceinline__ dd dd_add(dd a, dd b) {
+    const dd s = two_sum(a.hi, b.hi);
+    return quick_two_sum(s.hi, s.lo + (a.lo + b.lo));
+}
+__device__ __forceinline__ dd dd_neg(dd a) { return {-a.hi, -a.lo}; }
+__device__ __forceinline__ dd dd_mul(dd a, double b) {
+    const dd p = two_prod(a.hi, b);
+    return quick_two_sum(p.hi, __builtin_fma(a.lo, b, p.lo));
+}
+__device__ __forceinline__ dd dd_mul(dd a, dd b) {
+    const dd p = two_prod(a.hi, b.hi);
+    return quick_two_sum(p.hi, __builtin_fma(a.hi, b.lo, __builtin_fma(a.lo, b.hi, p.lo)));
+}
+// c^e for a small non-negative integer e (ipow in double-double)
+__device__ __forceinline__ dd dd_pow(dd c, int e) {
+    dd r = dd_of(1.0);
+    for (int q = 0; q < e; ++q) r = dd_mul(r, c);
+    return r;
+}
+#pragma clang fp contract(fast)   // the build default (-ffp-contract=fast) again
+
 // Step-size factor of the error controller, 0.9 en^(-1/4) with en^2 = q the
 // mean squared scaled error, in fp32 (three single-instruction estimates
 // instead of the fp64 sqrt / rsqrt sequences: the factor needs ~3 digits).
@@ -230,11 +275,18 @@ __device__ __forceinline__ bool lu(double (&A)[NS][NS], int (&piv)[NS], unsigned
         piv[k] = p;
         if (__any(p != k)) {
             swaps |= 1u << k;
+            // the trailing columns only (LINPACK's dgefa): the multipliers of
+            // the earlier columns stay in the rows they were computed in, which
+            // is what lu_solve's forward sweep -- swap b[k], then eliminate
+            // with column k -- assumes.  Rounds 1-4 swapped whole rows here
+            // (LAPACK's storage, whose solve applies every swap first), so a
+            // swap at column k >= 1 left the solve with a wrong L: 95 % of
+            // random 5 x 5 systems solved to O(1) error (DESIGN.md "LU").
 #pragma unroll
             for (int r = k + 1; r < NS; ++r) {
                 const bool sw = (p == r);
 #pragma unroll
-                for (int q = 0; q < NS; ++q) {
+                for (int q = k; q < NS; ++q) {
                     const double a = A[k][q], b = A[r][q];
                     A[k][q] = sw ? b : a;
                     A[r][q] = sw ? a : b;

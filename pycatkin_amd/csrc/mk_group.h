@@ -173,6 +173,25 @@ __device__ __forceinline__ int gmaxi(int v) {
     PCK_ROW_REDUCE(v, op_maxi, dppi);
     return grows<G>(v, op_maxi);
 }
+// group sum in double-double (the Newton refinement's conservation rows);
+// dd_add is commutative bit for bit, so every lane gets the same value
+template <int CTRL>
+__device__ __forceinline__ dd dppdd(dd v) { return {dppd<CTRL>(v.hi), dppd<CTRL>(v.lo)}; }
+template <int G>
+__device__ __forceinline__ dd gsum_dd(dd v) {
+    v = dd_add(v, dppdd<0xB1>(v));
+    v = dd_add(v, dppdd<0x4E>(v));
+    v = dd_add(v, dppdd<0x141>(v));
+    v = dd_add(v, dppdd<0x140>(v));
+    if constexpr (G == 16) {
+        return v;
+    } else {
+        const dd a{rlane(v.hi, 0), rlane(v.lo, 0)}, b{rlane(v.hi, 16), rlane(v.lo, 16)};
+        const dd c{rlane(v.hi, 32), rlane(v.lo, 32)}, d{rlane(v.hi, 48), rlane(v.lo, 48)};
+        if constexpr (G == 64) return dd_add(dd_add(a, b), dd_add(c, d));
+        return (threadIdx.x & 32) ? dd_add(c, d) : dd_add(a, b);
+    }
+}
 
 // lane K (compile-time after unrolling) of every row of 16: DPP row_newbcast
 __device__ __forceinline__ double bc16(double v, int k) {
@@ -575,6 +594,56 @@ __device__ __forceinline__ double ct_rhs(const Grp<NSP>& x, double y, double* gr
     return f * x.rs + x.fl * (x.in - y);
 }
 
+// the calling lane's row f in double-double, rounded once (mk_solver.h:
+// rhs_dd; the Newton refinement's residual): concentrations as exact
+// products cf_q y_q of the group's raw states, every reaction's rates and
+// their difference error-free, one reaction per scheduling region
+template <class Net, int NSP, int G>
+__device__ __forceinline__ double ct_rhs_dd(const Grp<NSP>& x, double y) {
+    constexpr int NS = Net::NS, R = Net::R;
+    ct_reload();
+    const int gl = ct_row(x.gl);
+    if constexpr (G == 64) {
+        wsync();
+        if (x.row) x.c[x.gl] = y;                  // the raw state (put_c rewrites c before its next use)
+        wsync();
+    }
+    // c_q = cf_q y_q exactly, fetched where a reaction uses it: the state
+    // passes through an empty asm per reaction, so the broadcasts are not
+    // shared across reactions (holding all NS concentrations in double-double
+    // would cost 4 NS VGPRs: CH4 went to 256 with 4 spilled)
+    dd acc = dd_of(0.0);
+    sfor<0, R>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        if constexpr (ct_col_used<Net, j>()) {
+            double yv = y;
+            asm volatile("" : "+v"(yv));
+            auto conc = [&](auto qc) {
+                constexpr int q = decltype(qc)::value;
+                if constexpr (G == 64) return two_prod(Net::dyn(q, 0), ((lds_cdouble*)x.c)[q]);
+                else return two_prod(Net::dyn(q, 0), gbcast_k<G>(yv, q));
+            };
+            dd rf = dd_of(ct_k(x.kf, j)), rr = dd_of(ct_k(x.kr, j));
+            sfor<0, NS>([&](auto ic) {
+                constexpr int i = decltype(ic)::value;
+                if constexpr (Net::ef(j, i) > 0 || Net::er(j, i) > 0) {
+                    const dd ci = conc(ic);
+                    if constexpr (Net::ef(j, i) > 0) rf = dd_mul(rf, dd_pow(ci, Net::ef(j, i)));
+                    if constexpr (Net::er(j, i) > 0) rr = dd_mul(rr, dd_pow(ci, Net::er(j, i)));
+                }
+            });
+            acc = dd_add(acc, dd_mul(dd_add(rf, dd_neg(rr)), ct_coef<Net, j>(gl)));
+            // the running sum passes through an empty asm (ct_fence): each
+            // reaction is finished before the next one's loads issue
+            asm volatile("" : "+v"(acc.hi), "+v"(acc.lo) :: "memory");
+        }
+    });
+    if (!x.row) return 0.0;
+    dd r = dd_mul(acc, x.rs);
+    if (x.fl != 0.0) r = dd_add(r, dd_mul(two_sum(x.in, -y), x.fl));
+    return r.hi + r.lo;
+}
+
 // d(prod_i c_i^E(J, i)) / d y_Q, times k (mk_solver.h: jac)
 template <class Net, int J, int Q, bool FWD>
 __device__ __forceinline__ double ct_dside(double k, const double (&c)[Net::NS]) {
@@ -692,6 +761,64 @@ __device__ __forceinline__ double grp_rhs(const GrpView& g, const Grp<NSP>& x, d
         f = (f + f2) * x.rs + x.fl * (x.in - y);
     }
     return f;
+}
+
+// The row's f in double-double (ct_rhs_dd) for the record-table kernels:
+// lane-per-reaction rates in double-double, their high parts gathered along
+// the species CSR with error-free products and sums, then their low parts
+// (the per-row loops, also where the balanced walk is compiled in: this runs
+// a few times per solve)
+template <int NSP, int G>
+__device__ __forceinline__ double tab_rhs_dd(const NetView& nv, const GrpView& g, const Grp<NSP>& x, double y) {
+    wsync();
+    if (x.row) x.c[x.gl] = y;                      // the raw state (put_c rewrites c before its next use)
+    wsync();
+    auto rate = [&](int r) {
+        const uint4 rec = g.rx[r];
+        dd a = dd_of(x.kf[r]), b = dd_of(x.kr[r]);
+#pragma unroll
+        for (int k = 0; k < PCK_GRP_NPMAX; ++k) {
+            const int f = rx_field(rec, k);
+            const int q = f & 63, ef = (f >> 6) & 31, er = f >> 11;
+            if (ef | er) {
+                const dd cq = two_prod(nv.dyn[4 * q], x.c[q]);
+                if (ef) a = dd_mul(a, dd_pow(cq, ef));
+                if (er) b = dd_mul(b, dd_pow(cq, er));
+            }
+        }
+        return dd_add(a, dd_neg(b));
+    };
+    for (int r = x.gl; r < x.R; r += G) x.d[r] = rate(r).hi;
+    wsync();
+    dd acc = dd_of(0.0);
+    if (x.row) {
+        for (int e = x.rb; e < x.re; ++e) {
+            const uint4 q = g.ent[e];
+            acc = dd_add(acc, two_prod(ent_s(q), x.d[ent_r(q)]));
+        }
+    }
+    wsync();
+    for (int r = x.gl; r < x.R; r += G) x.d[r] = rate(r).lo;
+    wsync();
+    if (x.row) {
+        double lo = 0.0;
+        for (int e = x.rb; e < x.re; ++e) {
+            const uint4 q = g.ent[e];
+            lo = fma(ent_s(q), x.d[ent_r(q)], lo);
+        }
+        acc = dd_add(acc, dd_of(lo));
+    }
+    wsync();
+    if (!x.row) return 0.0;
+    dd r = dd_mul(acc, x.rs);
+    if (x.fl != 0.0) r = dd_add(r, dd_mul(two_sum(x.in, -y), x.fl));
+    return r.hi + r.lo;
+}
+
+template <int NSP, int G, class Net = NoNet>
+__device__ __forceinline__ double grp_rhs_dd(const NetView& nv, const GrpView& g, const Grp<NSP>& x, double y) {
+    if constexpr (IsCt<Net>::v) return ct_rhs_dd<Net, NSP, G>(x, y);
+    else return tab_rhs_dd<NSP, G>(nv, g, x, y);
 }
 
 // W[q] = sgn * dF_i/dy_q + (q == i ? shift : 0), with dF/dy including the flow
@@ -1044,16 +1171,18 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
     // (1e11 / s on DMTM), and the stage solve multiplies it by h g along the
     // Jacobian's null direction -- at h ~ 1e9 s on a steady state that drift
     // swamps the tolerance and the step is rejected over and over.  The
-    // drift is removed along y (the direction of the multiplicative
-    // projection after the step, so a species' correction scales with its
-    // size); an orthogonal projection spreads the large species' rounding
-    // onto the tiny ones and stalls the solve (tools/rodas_mirror.py KPROJ).
-    double icy[PCK_MAX_CONS];
+    // drift is removed along y restricted to the law's own species (the
+    // direction of the multiplicative projection after the step, so a
+    // species' correction scales with its size, and a species outside the law
+    // -- a CSTR gas, another site type -- is left alone); an orthogonal
+    // projection spreads the large species' rounding onto the tiny ones and
+    // stalls the solve (tools/rodas_mirror.py KPROJ).
+    double icy[PCK_MAX_CONS];                  // this lane's y / (c . y) on the law's species, else 0
     auto kproj = [&](double k) {
         if (PCK_GRP_KPROJ && !crows) {
 #pragma unroll
             for (int l = 0; l < PCK_MAX_CONS; ++l)
-                if (l < nv.NCONS && cpos[l]) k -= gsum<G>(ci[l] * k) * icy[l] * y;
+                if (l < nv.NCONS && cpos[l]) k -= gsum<G>(ci[l] * k) * icy[l];
         }
         return k;
     };
@@ -1122,7 +1251,7 @@ __device__ __forceinline__ int grp_integrate(const NetView& nv, const GrpView& g
             for (int l = 0; l < PCK_MAX_CONS; ++l) {
                 if (l < nv.NCONS && cpos[l]) {
                     const double cy = gsum<G>(ci[l] * y);
-                    icy[l] = (cy > 0.0) ? 1.0 / cy : 0.0;
+                    icy[l] = (cy > 0.0 && ci[l] != 0.0) ? y / cy : 0.0;
                 }
             }
         }
@@ -1325,6 +1454,7 @@ __device__ __forceinline__ int grp_newton(const NetView& nv, const GrpView& gv, 
         }
     }
     double z = y, z_prev = y, bal_prev = INFINITY;
+    double scl = 1.0;                          // this row's scale in the last factorisation (F)
     bool conv = false;
     double prev = INFINITY, lastq = 1.0;
     int linear = 0;
@@ -1351,10 +1481,10 @@ __device__ __forceinline__ int grp_newton(const NetView& nv, const GrpView& gv, 
         double m = 0.0;
 #pragma unroll
         for (int q = 0; q < NSP; ++q) m = fmax(m, fabs(F.W[q]));
-        const double sc = (m > 0.0) ? 1.0 / m : 1.0;
+        scl = (m > 0.0) ? 1.0 / m : 1.0;
 #pragma unroll
-        for (int q = 0; q < NSP; ++q) F.W[q] *= sc;
-        Gv = -Gv * sc;
+        for (int q = 0; q < NSP; ++q) F.W[q] *= scl;
+        Gv = -Gv * scl;
         if (!grp_lu<NSP, G>(x, F)) break;
         double dz = grp_solve<NSP, G>(x, F, Gv);
         double alpha = 1.0;
@@ -1377,6 +1507,43 @@ __device__ __forceinline__ int grp_newton(const NetView& nv, const GrpView& gv, 
         prev = rel;
     }
     if (!conv) return PCK_ST_NEWTON;
+    if (PCK_NEWTON_REFINE > 0) {
+        // residual refinement (mk_solver.h: newton), on the loop's last
+        // factorisation (F) and row scale: a second Jacobian and LU in this
+        // kernel took CH4 from 197 to 256 VGPRs and DMTM from 3 to 2 waves
+        // per SIMD.  A Jacobian one step old converges linearly at a rate of
+        // that step times the condition; steps above PCK_REFINE_MAXSTEP are
+        // refused.
+        double nprev = INFINITY, zp = z;
+#pragma unroll 1
+        for (int r = 0; r <= PCK_NEWTON_REFINE; ++r) {
+            double Gv = grp_rhs_dd<NSP, G, Net>(nv, gv, x, z);
+#pragma unroll
+            for (int l = 0; l < PCK_MAX_CONS; ++l) {
+                if (l < nv.NCONS) {
+                    const dd s = dd_add(gsum_dd<G>(two_prod(ci[l], z)), dd_of(-b[l]));
+                    if (x.gl == piv_l[l]) Gv = s.hi + s.lo;
+                }
+            }
+            Gv = -Gv * scl;
+            const double nr = gmax<G>(x.row ? fabs(Gv) : 0.0);
+            if (!(nr < nprev)) {                        // no longer falling: the previous iterate
+                if (r > 0) z = zp;
+                break;
+            }
+            nprev = nr;
+            if (r == PCK_NEWTON_REFINE || nr == 0.0) break;
+            const double dz = grp_solve<NSP, G>(x, F, Gv);
+            const double zmax = gmax<G>(x.row ? fabs(z) : 0.0);
+            const double rel = gmax<G>(x.row ? fabs(dz) / fmax(fabs(z), 1e-12 * zmax + 1e-300) : 0.0);
+            zp = z;
+            z += dz;
+            if (!(gmin<G>((!x.row || isfinite(z)) ? 1.0 : 0.0) > 0.0) || !(rel <= PCK_REFINE_MAXSTEP)) {
+                z = zp;
+                break;
+            }
+        }
+    }
     if (gmin<G>((x.row && z < 0.0) ? -1.0 : 1.0) < 0.0) return PCK_ST_NEWTON;
     if (!grp_resolved<NSP, G, Net>(nv, gv, x, z)) return PCK_ST_NEWTON;   // converged in absolute terms only
     // mk_solver.h: newton -- the root only if the transient end reached it
@@ -1478,6 +1645,14 @@ template <int NSP, int G, int P, bool TRAJ = false, bool TAB = false, class Net 
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 64 ? PCK_GRP_WAVES : PCK_GRP_WAVES16))) k_solve_grp(NetView nv, GrpView gv, CondView cv, const double* kf,
                                                   const double* kr, int64_t ld_k, SolveArgs a, GrpArgs ga) {
     extern __shared__ double lds[];
+#if PCK_POISON_LDS
+    {   // diagnostic builds: the whole dynamic LDS block starts as NaN (mk_solver.h: k_solve)
+        const size_t nd = (TAB ? grp_tab_doubles(nv.NRXN, gv.NE, nv.NDYN, gv.LS * G) : 0) +
+                          (size_t)(64 / G) * grp_lds_doubles(nv.NRXN, NSP, nv.NDYN, gv.ND, ga.QB, gv.LS, gv.NX);
+        for (size_t i = threadIdx.x; i < nd; i += 64) lds[i] = __builtin_nan("");
+        wsync();
+    }
+#endif
     const int grp = threadIdx.x / G;
     const int64_t v = (int64_t)blockIdx.x * (64 / G) + grp;
     const int64_t slot = cond_of(a, v, ga.M, cv.n);
@@ -1551,14 +1726,17 @@ __global__ void __launch_bounds__(256) k_drc_combine(int64_t n, int R, double ep
     const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= n) return;
     const double t0 = tofbuf[c];
-    int st = stbuf[c];
+    int st = stbuf[c], stmin = st;
     int ns = nsbuf[c];
     for (int j = 0; j < R; ++j) {
         const double tp = tofbuf[(int64_t)(2 * j + 1) * n + c], tm = tofbuf[(int64_t)(2 * j + 2) * n + c];
         xi[j * ld_xi + c] = (tp - tm) / (2.0 * eps * t0);
-        st = max(st, max(stbuf[(int64_t)(2 * j + 1) * n + c], stbuf[(int64_t)(2 * j + 2) * n + c]));
+        const int sp = stbuf[(int64_t)(2 * j + 1) * n + c], sm = stbuf[(int64_t)(2 * j + 2) * n + c];
+        st = max(st, max(sp, sm));
+        stmin = min(stmin, min(sp, sm));
         ns += nsbuf[(int64_t)(2 * j + 1) * n + c] + nsbuf[(int64_t)(2 * j + 2) * n + c];
     }
+    st = drc_status(st, stmin);
     // a zero or non-finite base TOF makes every xi meaningless
     if (st == PCK_ST_OK && !(isfinite(t0) && t0 != 0.0)) st = PCK_ST_NONFINITE;
     if (tof0) tof0[c] = t0;

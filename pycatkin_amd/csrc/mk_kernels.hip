@@ -172,6 +172,20 @@ extern "C" int pck_trace_get(double* host, int* pos) {
     return PCK_OK;
 }
 #endif
+#if PCK_PHASE
+// diagnostic builds only (-DPCK_PHASE=1): the lane integrator's phase
+// counters (mk_solver.h: PCK_LPH), zeroed / read by tools/phase_lane.py
+extern "C" int pck_lphase_reset(void) {
+    const double z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(pck_lphase), z, sizeof(z)));
+    return PCK_OK;
+}
+extern "C" int pck_lphase_get(double* host8) {
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpyFromSymbol(host8, HIP_SYMBOL(pck_lphase), sizeof(double) * 8));
+    return PCK_OK;
+}
+#endif
 extern "C" const char* pck_last_error(void) { return g_err; }
 
 extern "C" int pck_network_create(const int32_t* ip, int64_t n_ip, const double* dp, int64_t n_dp,
@@ -666,9 +680,16 @@ extern "C" int pck_species_rates(const pck_network* net, const pck_conditions* c
     const int B = 128;
     const size_t shm = lds_bytes(net->nv.NRXN, net->nv.NDYN, B);
     dim3 g((unsigned)((n + B - 1) / B));
-#define CALL(N) hipLaunchKernelGGL(k_species_rates<N>, g, dim3(B), shm, (hipStream_t)stream, net->nv, cview(cond), kf, kr, ld_k, y, ld_y, dydt)
-    PCK_NS_SWITCH(net->nv.NDYN, CALL)
+    const char* edd = getenv("PCK_RATES_DD");     // diagnostics: the double-double residual of the Newton refinement
+    if (edd && edd[0] == '1') {
+#define CALL(N) hipLaunchKernelGGL((k_species_rates<N, true>), g, dim3(B), shm, (hipStream_t)stream, net->nv, cview(cond), kf, kr, ld_k, y, ld_y, dydt)
+        PCK_NS_SWITCH(net->nv.NDYN, CALL)
 #undef CALL
+    } else {
+#define CALL(N) hipLaunchKernelGGL((k_species_rates<N, false>), g, dim3(B), shm, (hipStream_t)stream, net->nv, cview(cond), kf, kr, ld_k, y, ld_y, dydt)
+        PCK_NS_SWITCH(net->nv.NDYN, CALL)
+#undef CALL
+    }
     HIPCHK(hipGetLastError());
     return PCK_OK;
 }

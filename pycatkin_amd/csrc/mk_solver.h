@@ -28,6 +28,72 @@ __device__ int pck_trace_pos = 0;
 __device__ double pck_trace_buf[PCK_TRACE_N * PCK_TRACE_W];
 #endif
 
+// Phase split of the lane integrator (diagnostic builds, -DPCK_PHASE=1;
+// tools/phase_lane.py): shader-clock cycles of the waves whose block index
+// is a multiple of PCK_PHASE_EVERY, per phase of a step, summed over those
+// waves (lane 0 adds them up at the end of the solve):
+//   [0 Jacobian + W, 1 LU, 2 six solves, 3 seven rhs, 4 stage combinations,
+//    5 error norm / controller / projection / bookkeeping, 6 steps, 7 waves]
+// Scheduling barriers around every stamp keep the phases in sequence; they
+// cost the build its cross-phase overlap, so absolute cycles read high.
+#ifndef PCK_PHASE
+#define PCK_PHASE 0
+#endif
+#ifndef PCK_PHASE_EVERY
+#define PCK_PHASE_EVERY 64
+#endif
+#if PCK_PHASE
+__device__ double pck_lphase[8];
+#define PCK_LPH_DECL                                                                   \
+    double lph[8] = {0, 0, 0, 0, 0, 0, 0, 0};                                          \
+    const bool lph_on = (blockIdx.x % PCK_PHASE_EVERY) == 0;                           \
+    long long lph_t = 0
+#define PCK_LPH(i, ...)                                                                \
+    do {                                                                               \
+        __builtin_amdgcn_sched_barrier(0);                                             \
+        const long long t_ph0 = __builtin_readcyclecounter();                          \
+        __builtin_amdgcn_sched_barrier(0);                                             \
+        __VA_ARGS__;                                                                   \
+        __builtin_amdgcn_sched_barrier(0);                                             \
+        if (lph_on) lph[i] += (double)(__builtin_readcyclecounter() - t_ph0);          \
+        __builtin_amdgcn_sched_barrier(0);                                             \
+    } while (0)
+#define PCK_LPH_STEP() do { if (lph_on) lph[6] += 1.0; } while (0)
+#define PCK_LPH_MARK()                                                                 \
+    do {                                                                               \
+        __builtin_amdgcn_sched_barrier(0);                                             \
+        lph_t = __builtin_readcyclecounter();                                          \
+        __builtin_amdgcn_sched_barrier(0);                                             \
+    } while (0)
+#define PCK_LPH_UNTIL(i)                                                               \
+    do {                                                                               \
+        __builtin_amdgcn_sched_barrier(0);                                             \
+        const long long t_ph1 = __builtin_readcyclecounter();                          \
+        if (lph_on && lph_t) lph[i] += (double)(t_ph1 - lph_t);                        \
+        lph_t = 0;                                                                     \
+        __builtin_amdgcn_sched_barrier(0);                                             \
+    } while (0)
+#define PCK_LPH_FLUSH()                                                                \
+    do {                                                                               \
+        if (lph_on && (threadIdx.x & 63) == 0) {                                       \
+            lph[7] = 1.0;                                                              \
+            for (int q = 0; q < 8; ++q) atomicAdd(&pck_lphase[q], lph[q]);             \
+        }                                                                              \
+    } while (0)
+#else
+#define PCK_LPH_DECL
+#define PCK_LPH(i, ...) __VA_ARGS__
+#define PCK_LPH_STEP() do {} while (0)
+#define PCK_LPH_MARK() do {} while (0)
+#define PCK_LPH_UNTIL(i) do {} while (0)
+#define PCK_LPH_FLUSH() do {} while (0)
+#endif
+#define PCK_LRET(st)       \
+    do {                   \
+        PCK_LPH_FLUSH();   \
+        return st;         \
+    } while (0)
+
 template <int NS_>
 struct PlanRT {
     static constexpr int NS = NS_;
@@ -214,6 +280,11 @@ __host__ __device__ inline size_t lds_bytes(int R, int NS, int B) {
     return sizeof(double) * (size_t)(2 * (R > 0 ? R : 1) + NS) * B;
 }
 
+// every inflow slot is written (0 on rows without flow): PCK_INS_ALL=0 writes
+// only the flow rows (the round-4 code, A/B)
+#ifndef PCK_INS_ALL
+#define PCK_INS_ALL 1
+#endif
 template <class P>
 __device__ __forceinline__ void lane_setup(const P& p, const NetView& nv, const CondView& cv, int64_t c,
                                            Lane<P::NS>& L, double* lds_lane, int ks) {
@@ -226,7 +297,8 @@ __device__ __forceinline__ void lane_setup(const P& p, const NetView& nv, const 
     L.ins = ins;
 #pragma unroll
     for (int i = 0; i < P::NS; ++i)  // 1/residence_time on CSTR gas rows (reactor.py:154-156)
-        if (p.fl(i) != 0.0) ins[i * ks] = cv.inflow ? cv.inflow[i * cv.ld_in + c * cv.s_in] : 0.0;
+        if (PCK_INS_ALL || p.fl(i) != 0.0)
+            ins[i * ks] = (cv.inflow && p.fl(i) != 0.0) ? cv.inflow[i * cv.ld_in + c * cv.s_in] : 0.0;
 }
 
 // effective k (fixed species folded in, optional DRC perturbation)
@@ -316,6 +388,10 @@ __device__ __forceinline__ void cons_zero(const P& p, double (&b)[NS]) {
 // volcano step); the lane-group solver reads PCK_CONS_ROWS=1 at run time.
 #ifndef PCK_CONS_ROWS
 #define PCK_CONS_ROWS 0
+#endif
+// diagnostic builds: poison the dynamic LDS block at kernel start
+#ifndef PCK_POISON_LDS
+#define PCK_POISON_LDS 0
 #endif
 // integrate / newton are inlined into the kernel (see DESIGN.md "Runtime-plan
 // fault"); -DPCK_LANE_INLINE=__noinline__ builds the call variant for study
@@ -412,6 +488,7 @@ __device__ PCK_LANE_INLINE int integrate(const P& p, const Lane<P::NS>& L, const
                          const TrajOut& to) {
     using namespace rodas4;
     constexpr int NS = P::NS;
+    PCK_LPH_DECL;
     int ko = 0;
     if constexpr (TRAJ) {
         for (; ko < to.n && to.t[ko] <= t0; ++ko) {
@@ -428,7 +505,7 @@ __device__ PCK_LANE_INLINE int integrate(const P& p, const Lane<P::NS>& L, const
                 for (int i = 0; i < NS; ++i) to.y[((int64_t)ko * NS + i) * to.ld + to.c] = y[i];
             }
         }
-        return PCK_ST_OK;
+        PCK_LRET(PCK_ST_OK);
     }
     double F0[NS];
     rhs(p, L, k, y, F0);
@@ -474,58 +551,51 @@ __device__ PCK_LANE_INLINE int integrate(const P& p, const Lane<P::NS>& L, const
     int blowups = 0;
     int stall = 0;
     while (t < t_end) {
-        if (__builtin_amdgcn_readfirstlane(nsteps) >= max_steps) return PCK_ST_MAXSTEPS;
+        if (__builtin_amdgcn_readfirstlane(nsteps) >= max_steps) PCK_LRET(PCK_ST_MAXSTEPS);
         ++nsteps;
+        PCK_LPH_STEP();
         bool last = false;
         if (t + h >= t_end) { h = t_end - t; last = true; }
-        jac(p, L, k, y, W);                               // W = I/(h g) - J
-        const double ih = rcp(h);
-        const double ig = ih * (1.0 / g);
-#pragma unroll
-        for (int i = 0; i < NS; ++i) {
-#pragma unroll
-            for (int q = 0; q < NS; ++q) W[i][q] = -W[i][q];
-            W[i][i] += ig;
-        }
+        double ih, ig;
+        PCK_LPH(0, jac(p, L, k, y, W);                               // W = I/(h g) - J
+               ih = rcp(h); ig = ih * (1.0 / g);
+               for (int i = 0; i < NS; ++i) {
+                   for (int q = 0; q < NS; ++q) W[i][q] = -W[i][q];
+                   W[i][i] += ig;
+               });
         if (PCK_CONS_ROWS && crows) cons_rows(p, W);
-        if (!lu<NS>(W, piv, sw)) {
+        bool luok;
+        PCK_LPH(1, luok = lu<NS>(W, piv, sw));
+        if (!luok) {
             h *= 0.25;
-            if (!(h > 2.220446049250313e-15 * fmax(fabs(t), 1e-300))) return PCK_ST_STEPFAIL;
+            if (!(h > 2.220446049250313e-15 * fmax(fabs(t), 1e-300))) PCK_LRET(PCK_ST_STEPFAIL);
             continue;
         }
         double k1[NS], k2[NS], k3[NS], k4[NS], k5[NS], u[NS], fu[NS];
 #pragma unroll
         for (int i = 0; i < NS; ++i) k1[i] = F0[i];
         if (PCK_CONS_ROWS && crows) cons_zero(p, k1);
-        lu_solve<NS>(W, piv, sw, k1);
-#pragma unroll
-        for (int i = 0; i < NS; ++i) u[i] = y[i] + a21 * k1[i];
-        rhs(p, L, k, u, fu);
-#pragma unroll
-        for (int i = 0; i < NS; ++i) k2[i] = fu[i] + ih * (C21 * k1[i]);
+        PCK_LPH(2, lu_solve<NS>(W, piv, sw, k1));
+        PCK_LPH(4, for (int i = 0; i < NS; ++i) u[i] = y[i] + a21 * k1[i]);
+        PCK_LPH(3, rhs(p, L, k, u, fu));
+        PCK_LPH(4, for (int i = 0; i < NS; ++i) k2[i] = fu[i] + ih * (C21 * k1[i]));
         if (PCK_CONS_ROWS && crows) cons_zero(p, k2);
-        lu_solve<NS>(W, piv, sw, k2);
-#pragma unroll
-        for (int i = 0; i < NS; ++i) u[i] = y[i] + a31 * k1[i] + a32 * k2[i];
-        rhs(p, L, k, u, fu);
-#pragma unroll
-        for (int i = 0; i < NS; ++i) k3[i] = fu[i] + ih * (C31 * k1[i] + C32 * k2[i]);
+        PCK_LPH(2, lu_solve<NS>(W, piv, sw, k2));
+        PCK_LPH(4, for (int i = 0; i < NS; ++i) u[i] = y[i] + a31 * k1[i] + a32 * k2[i]);
+        PCK_LPH(3, rhs(p, L, k, u, fu));
+        PCK_LPH(4, for (int i = 0; i < NS; ++i) k3[i] = fu[i] + ih * (C31 * k1[i] + C32 * k2[i]));
         if (PCK_CONS_ROWS && crows) cons_zero(p, k3);
-        lu_solve<NS>(W, piv, sw, k3);
-#pragma unroll
-        for (int i = 0; i < NS; ++i) u[i] = y[i] + a41 * k1[i] + a42 * k2[i] + a43 * k3[i];
-        rhs(p, L, k, u, fu);
-#pragma unroll
-        for (int i = 0; i < NS; ++i) k4[i] = fu[i] + ih * (C41 * k1[i] + C42 * k2[i] + C43 * k3[i]);
+        PCK_LPH(2, lu_solve<NS>(W, piv, sw, k3));
+        PCK_LPH(4, for (int i = 0; i < NS; ++i) u[i] = y[i] + a41 * k1[i] + a42 * k2[i] + a43 * k3[i]);
+        PCK_LPH(3, rhs(p, L, k, u, fu));
+        PCK_LPH(4, for (int i = 0; i < NS; ++i) k4[i] = fu[i] + ih * (C41 * k1[i] + C42 * k2[i] + C43 * k3[i]));
         if (PCK_CONS_ROWS && crows) cons_zero(p, k4);
-        lu_solve<NS>(W, piv, sw, k4);
-#pragma unroll
-        for (int i = 0; i < NS; ++i) u[i] = y[i] + a51 * k1[i] + a52 * k2[i] + a53 * k3[i] + a54 * k4[i];
-        rhs(p, L, k, u, fu);
-#pragma unroll
-        for (int i = 0; i < NS; ++i) k5[i] = fu[i] + ih * (C51 * k1[i] + C52 * k2[i] + C53 * k3[i] + C54 * k4[i]);
+        PCK_LPH(2, lu_solve<NS>(W, piv, sw, k4));
+        PCK_LPH(4, for (int i = 0; i < NS; ++i) u[i] = y[i] + a51 * k1[i] + a52 * k2[i] + a53 * k3[i] + a54 * k4[i]);
+        PCK_LPH(3, rhs(p, L, k, u, fu));
+        PCK_LPH(4, for (int i = 0; i < NS; ++i) k5[i] = fu[i] + ih * (C51 * k1[i] + C52 * k2[i] + C53 * k3[i] + C54 * k4[i]));
         if (PCK_CONS_ROWS && crows) cons_zero(p, k5);
-        lu_solve<NS>(W, piv, sw, k5);
+        PCK_LPH(2, lu_solve<NS>(W, piv, sw, k5));
         double d2[TRAJ ? NS : 1], d3[TRAJ ? NS : 1];
         if constexpr (TRAJ) {
             using namespace rodas4_dense;
@@ -535,15 +605,14 @@ __device__ PCK_LANE_INLINE int integrate(const P& p, const Lane<P::NS>& L, const
                 d3[i] = D3_K5_ONLY ? D35 * k5[i] : D31 * k1[i] + D32 * k2[i] + D33 * k3[i] + D34 * k4[i] + D35 * k5[i];
             }
         }
-#pragma unroll
-        for (int i = 0; i < NS; ++i) u[i] += k5[i];
-        rhs(p, L, k, u, fu);
+        PCK_LPH(4, for (int i = 0; i < NS; ++i) u[i] += k5[i]);
+        PCK_LPH(3, rhs(p, L, k, u, fu));
         // k6 reuses k5's registers once k5 is folded into u
-#pragma unroll
-        for (int i = 0; i < NS; ++i)
-            k5[i] = fu[i] + ih * (C61 * k1[i] + C62 * k2[i] + C63 * k3[i] + C64 * k4[i] + C65 * k5[i]);
+        PCK_LPH(4, for (int i = 0; i < NS; ++i)
+                       k5[i] = fu[i] + ih * (C61 * k1[i] + C62 * k2[i] + C63 * k3[i] + C64 * k4[i] + C65 * k5[i]));
         if (PCK_CONS_ROWS && crows) cons_zero(p, k5);
-        lu_solve<NS>(W, piv, sw, k5);
+        PCK_LPH(2, lu_solve<NS>(W, piv, sw, k5));
+        PCK_LPH_MARK();
         double s = 0.0, umin = INFINITY, usum = 0.0;
 #pragma unroll
         for (int i = 0; i < NS; ++i) {
@@ -601,7 +670,9 @@ __device__ PCK_LANE_INLINE int integrate(const P& p, const Lane<P::NS>& L, const
                             y_old[i] * s1 + sv * (y[i] + s1 * (d2[i] + sv * d3[i]));
                 }
             }
-            rhs(p, L, k, y, F0);
+            PCK_LPH_UNTIL(5);
+            PCK_LPH(3, rhs(p, L, k, y, F0));
+            PCK_LPH_MARK();
             // a tolerance-level negative (>= -atol) that is still falling is set
             // to 0: left alone, a mass-action term of order >= 2 keeps driving it
             // down and the positivity rule then shrinks h to nothing; clipping
@@ -631,17 +702,18 @@ __device__ PCK_LANE_INLINE int integrate(const P& p, const Lane<P::NS>& L, const
             } else {
                 h *= finite ? fmax(0.2, fac) : 0.25;
                 // repeated catastrophic rejections: see mk_group.h grp_integrate
-                if (!(q < PCK_BLOWUP_Q) && h < 1e-4 * t && ++blowups > PCK_MAX_BLOWUPS) return PCK_ST_STEPFAIL;
+                if (!(q < PCK_BLOWUP_Q) && h < 1e-4 * t && ++blowups > PCK_MAX_BLOWUPS) PCK_LRET(PCK_ST_STEPFAIL);
             }
         }
         // stagnation, sampled every PCK_STALL_EVERY steps (the active lanes of a
         // wave share the step counter: a scalar test)
         if ((__builtin_amdgcn_readfirstlane(nsteps) & (PCK_STALL_EVERY - 1)) == 0) {
             stall = (h < PCK_STALL_H * (t - t0)) ? stall + PCK_STALL_EVERY : 0;
-            if (stall > PCK_STALL_STEPS) return PCK_ST_STEPFAIL;
+            if (stall > PCK_STALL_STEPS) PCK_LRET(PCK_ST_STEPFAIL);
         }
         // scipy's BDF limit: a step below 10 ulp(t) is a failure
-        if (!(h > 2.220446049250313e-15 * fmax(fabs(t), 1e-300)) && t < t_end) return PCK_ST_STEPFAIL;
+        if (!(h > 2.220446049250313e-15 * fmax(fabs(t), 1e-300)) && t < t_end) PCK_LRET(PCK_ST_STEPFAIL);
+        PCK_LPH_UNTIL(5);
     }
     if constexpr (TRAJ) {
         // samples past t_end (a caller's log grid can round one ulp above it)
@@ -651,7 +723,7 @@ __device__ PCK_LANE_INLINE int integrate(const P& p, const Lane<P::NS>& L, const
             for (int i = 0; i < NS; ++i) to.y[((int64_t)ko * NS + i) * to.ld + to.c] = y[i];
         }
     }
-    return PCK_ST_OK;
+    PCK_LRET(PCK_ST_OK);
 }
 
 // Is y a root, not an artefact of Newton's absolute floor?  Every species
@@ -698,6 +770,42 @@ __device__ __forceinline__ void rhs_gross(const P& p, const Lane<P::NS>& L, cons
             f[i] += p.fl(i) * (L.ins[i * L.ks] - y[i]);
             g[i] += fabs(p.fl(i)) * (fabs(L.ins[i * L.ks]) + fabs(y[i]));
         }
+    }
+}
+
+// f in double-double (mk_device.h: dd), rounded once at the end: the
+// residual of the Newton refinement below.  The same terms as rhs; every
+// product and sum error-free, so the result carries the rounding of the
+// inputs (k_eff, the row scales, y) but not the cancellation of the fluxes.
+template <class P, class K>
+__device__ __forceinline__ void rhs_dd(const P& p, const Lane<P::NS>& L, const K& k, const double (&y)[P::NS],
+                                       double (&f)[P::NS]) {
+    constexpr int NS = P::NS;
+    dd c[NS], acc[NS];
+#pragma unroll
+    for (int i = 0; i < NS; ++i) { c[i] = two_prod(p.cf(i), y[i]); acc[i] = dd_of(0.0); }
+    for_rxn(p, [&](int j) {
+        dd rf = dd_of(k.f(j)), rr = dd_of(k.r(j));
+#pragma unroll
+        for (int i = 0; i < NS; ++i) {
+            if (p.ef(j, i)) rf = dd_mul(rf, dd_pow(c[i], p.ef(j, i)));
+            if (p.er(j, i)) rr = dd_mul(rr, dd_pow(c[i], p.er(j, i)));
+        }
+        const dd net = dd_add(rf, dd_neg(rr));
+#pragma unroll
+        for (int i = 0; i < NS; ++i) {
+            const double s = p.S(i, j);
+            if (s != 0.0) acc[i] = dd_add(acc[i], dd_mul(net, s));
+        }
+        // one reaction at a time (the ILP scheduler would interleave them all
+        // and raise the kernel's register count, i.e. lower its occupancy)
+        __builtin_amdgcn_sched_barrier(0);
+    });
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+        dd r = dd_mul(acc[i], (p.rsT(i) != 0.0) ? p.rs0(i) + p.rsT(i) * L.T : p.rs0(i));
+        if (p.fl(i) != 0.0) r = dd_add(r, dd_mul(two_sum(L.ins[i * L.ks], -y[i]), p.fl(i)));
+        f[i] = r.hi + r.lo;
     }
 }
 
@@ -759,6 +867,22 @@ __device__ __forceinline__ bool resolved(const P& p, const Lane<P::NS>& L, const
 // oracle's LAPACK solve happened to land inside 1e-12.
 #ifndef PCK_STEP_FLOOR
 #define PCK_STEP_FLOOR 1e-7
+#endif
+// Refinement of a converged root (mixed-precision iterative refinement):
+// Newton steps from the root with the residual in double-double (rhs_dd),
+// at most PCK_NEWTON_REFINE of them, stopped when the scaled residual stops
+// falling.  The plain iteration stops where the residual's rounding (eps x
+// the gross fluxes, amplified by a Jacobian condition up to 1e12) drowns the
+// step -- on a site-starved root that leaves ~1e-7 of the answer to the
+// rounding of one build, and two builds of one plan differed by 1.3e-6 in
+// TOF.  With the residual exact to ~eps^2 the steps converge to the root of
+// the rounded inputs in every well-determined direction, whatever order the
+// build evaluates the fluxes in.  0 turns it off (A/B).
+#ifndef PCK_NEWTON_REFINE
+#define PCK_NEWTON_REFINE 2
+#endif
+#ifndef PCK_REFINE_MAXSTEP
+#define PCK_REFINE_MAXSTEP 1e-6
 #endif
 
 // Newton on f(y) = 0 with the plan's conservation laws replacing their pivot
@@ -896,6 +1020,102 @@ __device__ PCK_LANE_INLINE int newton(const P& p, const Lane<P::NS>& L, const K&
     }
 #endif
     if (!conv) return PCK_ST_NEWTON;
+    if (PCK_NEWTON_REFINE > 0) {
+        // residual-refinement steps (PCK_NEWTON_REFINE): the Newton system of
+        // the loop above at the current iterate, its right-hand side in
+        // double-double.  Scheduling barriers keep the Jacobian / LU, the
+        // double-double residual and the solve in sequence (interleaved by
+        // the ILP scheduler they took the volcano kernel from 159 to 195
+        // VGPRs, two waves per SIMD instead of three).
+        double nprev = INFINITY;
+#pragma unroll 1
+        for (int r = 0; r <= PCK_NEWTON_REFINE; ++r) {
+            double J[NS][NS], sc[NS], G[NS];
+            int piv[NS];
+            unsigned sw;
+            jac(p, L, k, z, J);
+            for (int l = 0; l < p.ncons(); ++l) {
+                const int pv = p.cpiv(l);
+#pragma unroll
+                for (int i = 0; i < NS; ++i) {
+                    if (i == pv) {
+#pragma unroll
+                        for (int q = 0; q < NS; ++q) J[i][q] = p.C(l, q);
+                    }
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < NS; ++i) {
+                double m = 0.0;
+#pragma unroll
+                for (int q = 0; q < NS; ++q) m = fmax(m, fabs(J[i][q]));
+                sc[i] = (m > 0.0) ? 1.0 / m : 1.0;
+#pragma unroll
+                for (int q = 0; q < NS; ++q) J[i][q] *= sc[i];
+            }
+            const bool luok = lu<NS, true>(J, piv, sw);
+            __builtin_amdgcn_sched_barrier(0);
+            rhs_dd(p, L, k, z, G);
+            for (int l = 0; l < p.ncons(); ++l) {
+                const int pv = p.cpiv(l);
+                dd s = dd_of(-b[l]);
+#pragma unroll
+                for (int i = 0; i < NS; ++i) s = dd_add(s, two_prod(p.C(l, i), z[i]));
+#pragma unroll
+                for (int i = 0; i < NS; ++i)
+                    if (i == pv) G[i] = s.hi + s.lo;
+            }
+            double nr = 0.0;
+#pragma unroll
+            for (int i = 0; i < NS; ++i) {
+                G[i] = -G[i] * sc[i];
+                nr = fmax(nr, fabs(G[i]));
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#ifdef PCK_TRACE
+            if (L.cidx == pck_trace_cond) {           // refinement record: [100 + r, nr, luok, z0..z4]
+                double* rec = pck_trace_buf + (size_t)(pck_trace_pos % PCK_TRACE_N) * PCK_TRACE_W;
+                rec[0] = 100 + r; rec[1] = nr; rec[2] = luok ? 1.0 : 0.0;
+#pragma unroll
+                for (int i = 0; i < NS && i < PCK_TRACE_W - 3; ++i) rec[3 + i] = z[i];
+                pck_trace_pos = pck_trace_pos + 1;
+                double* rg = pck_trace_buf + (size_t)(pck_trace_pos % PCK_TRACE_N) * PCK_TRACE_W;
+                rg[0] = 200 + r; rg[1] = sw; rg[2] = 0.0;         // [200 + r, swaps, 0, G0..G4 (scaled)]
+#pragma unroll
+                for (int i = 0; i < NS && i < PCK_TRACE_W - 3; ++i) rg[3 + i] = G[i];
+                pck_trace_pos = pck_trace_pos + 1;
+            }
+#endif
+            if (!(nr < nprev)) {                         // no longer falling: the previous iterate
+                if (r > 0) {
+#pragma unroll
+                    for (int i = 0; i < NS; ++i) z[i] = z_prev[i];
+                }
+                break;
+            }
+            nprev = nr;
+            if (r == PCK_NEWTON_REFINE || nr == 0.0 || !luok) break;
+            lu_solve<NS>(J, piv, sw, G);
+            bool fin = true;
+            double zmax = 0.0, rel = 0.0;
+#pragma unroll
+            for (int i = 0; i < NS; ++i) zmax = fmax(zmax, fabs(z[i]));
+#pragma unroll
+            for (int i = 0; i < NS; ++i) {
+                z_prev[i] = z[i];
+                rel = fmax(rel, fabs(G[i]) / fmax(fabs(z[i]), 1e-12 * zmax + 1e-300));
+                z[i] += G[i];
+                fin = fin && isfinite(z[i]);
+            }
+            // a refinement moves a converged root by rounding, not by 1e-6:
+            // a larger step is the ill-conditioned direction speaking
+            if (!fin || !(rel <= PCK_REFINE_MAXSTEP)) {
+#pragma unroll
+                for (int i = 0; i < NS; ++i) z[i] = z_prev[i];
+                break;
+            }
+        }
+    }
 #pragma unroll
     for (int i = 0; i < NS; ++i)
         if (z[i] < 0.0) return PCK_ST_NEWTON;
@@ -938,7 +1158,7 @@ __device__ __forceinline__ double lane_tof(const P& p, const NetView& nv, const 
 // ---------------------------------------------------------------------------
 // evaluation kernels (runtime plans): pck_species_rates / pck_jacobian
 // ---------------------------------------------------------------------------
-template <int NS>
+template <int NS, bool DD = false>
 __global__ void __launch_bounds__(128) k_species_rates(NetView nv, CondView cv, const double* kf, const double* kr,
                                                        int64_t ld_k, const double* y, int64_t ld_y, double* dydt) {
     extern __shared__ double lds[];
@@ -952,7 +1172,10 @@ __global__ void __launch_bounds__(128) k_species_rates(NetView nv, CondView cv, 
     double yy[NS], f[NS];
 #pragma unroll
     for (int i = 0; i < NS; ++i) yy[i] = y[i * ld_y + c];
-    rhs(p, L, k, yy, f);
+    if constexpr (DD)
+        rhs_dd(p, L, k, yy, f);           // the Newton refinement's residual (diagnostics: PCK_RATES_DD=1)
+    else
+        rhs(p, L, k, yy, f);
 #pragma unroll
     for (int i = 0; i < NS; ++i) dydt[i * ld_y + c] = f[i];
 }
@@ -1021,6 +1244,14 @@ __device__ __forceinline__ int solve_lane(const P& p, const Lane<P::NS>& L, cons
     return st;
 }
 
+// a DRC condition's status from the worst and the best of its 2R+1 solves:
+// reached roots mixed with transient ends (the steady rule's two answers) are
+// PCK_ST_DRC_MIXED; any integrator failure (1-3) stays the worst status
+__host__ __device__ inline int drc_status(int worst, int best) {
+    return ((worst == PCK_ST_NEWTON || worst == PCK_ST_NEWTON_LOOSE) && best == PCK_ST_OK) ? PCK_ST_DRC_MIXED
+                                                                                          : worst;
+}
+
 // condition of a lane (or lane group) v: v / G, or the retry list's entry
 // (cv.n past the list's end: the lane idles)
 __device__ __forceinline__ int64_t cond_of(const SolveArgs& a, int64_t v, int G, int64_t n) {
@@ -1054,6 +1285,14 @@ __global__ void __launch_bounds__(PCK_SOLVE_BLOCK) __attribute__((amdgpu_waves_p
                                                int64_t ld_k, SolveArgs a) {
     constexpr int NS = P::NS;
     extern __shared__ double lds[];
+#if PCK_POISON_LDS
+    {   // diagnostic builds (-DPCK_POISON_LDS=1): the dynamic LDS block starts as
+        // NaN, so a read of an element no lane wrote this launch shows at once
+        const int nd = (2 * (nv.NRXN > 0 ? nv.NRXN : 1) + NS) * (int)blockDim.x;
+        for (int i = threadIdx.x; i < nd; i += blockDim.x) lds[i] = __builtin_nan("");
+        __syncthreads();
+    }
+#endif
     const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int G = a.G;
     const int64_t c = a.worder ? ((int64_t)a.worder[blockIdx.x] * PCK_SOLVE_BLOCK + threadIdx.x)
@@ -1117,11 +1356,14 @@ __global__ void __launch_bounds__(PCK_SOLVE_BLOCK) __attribute__((amdgpu_waves_p
         const double t0 = __shfl(tof, base, 64);
         const double tm = __shfl(tof, lane + 1 < 64 ? lane + 1 : lane, 64);
         int gst = active ? st : 0;
+        int gmin = active ? st : 1 << 20;
         int gns = active ? ns : 0;
         for (int m = 1; m < G; m <<= 1) {
             gst = max(gst, __shfl_xor(gst, m, 64));
+            gmin = min(gmin, __shfl_xor(gmin, m, 64));
             gns += __shfl_xor(gns, m, 64);
         }
+        gst = drc_status(gst, gmin);
         if (active && (q & 1)) {
             const int j = (q - 1) >> 1;
             a.xi[j * a.ld_xi + c] = (tof - tm) / (2.0 * a.eps * t0);   // old_system.py:508

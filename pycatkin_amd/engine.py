@@ -6,11 +6,15 @@ every number is computed by the HIP kernels of libpycatkin_amd.so.
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import numpy as np
 
 from . import _lib as L
 from .constants.physical_constants import bartoPa
+
+
+_POISON = os.environ.get('PCK_DEBUG_POISON') == '1'
 
 
 def _torch():
@@ -212,6 +216,11 @@ class DeviceNetwork:
             if want_k:
                 out['kf'] = torch.empty((self.NRXN, n), dtype=torch.float64, device='cuda')
                 out['kr'] = torch.empty_like(out['kf'])
+        if _POISON:
+            # diagnostics (PCK_DEBUG_POISON=1): every output starts as NaN / -7,
+            # so an element the kernels never write shows in the result
+            for k, v in out.items():
+                v.fill_(float('nan') if v.is_floating_point() else -7)
         o = L.Outputs()
         o.y, o.ld_y = _ptr(out['y']), n
         o.tof, o.status, o.nsteps = _ptr(out['tof']), _ptr(out['status']), _ptr(out['nsteps'])
@@ -240,15 +249,26 @@ class DeviceNetwork:
 _form_cache = {}
 
 
+def descriptor_values(dnames, T, desc=None):
+    """The descriptor column of one condition at temperature T: a
+    temperature-keyed user energy ('@T:' descriptor, energy.tkeyed) is looked
+    up in its table at T (KeyError on a missing T, like the reference's
+    dErxn_user[T], reaction.py:228-262); any other descriptor comes from
+    `desc` (ValueError if it is not given)."""
+    from .energy import TKEYED
+    given = [k for k in dnames if not k.startswith('@T:')]
+    if given and desc is None:
+        raise ValueError('forms depend on descriptors %s; pass desc=' % given)
+    return np.array([TKEYED[k][float(T)] if k.startswith('@T:') else desc[k] for k in dnames], float)
+
+
 def evaluate_forms(forms, T, p, states=None, desc=None):
     """Evaluate LinearForms (eV) for one condition on the device (kernel 1)."""
     from .network import compile_forms
     states_map = {s.name: s for s in (states or [])}
     ip, dp, regs, dnames = compile_forms(forms, states_map)
+    d = None if not dnames else descriptor_values(dnames, T, desc)
     net = DeviceNetwork(ip, dp)
-    if dnames and desc is None:
-        raise ValueError('forms depend on descriptors %s; pass desc=' % dnames)
-    d = None if not dnames else np.array([desc[k] for k in dnames], float)
     vals = net.energies(1, float(T), float(p), d).cpu().numpy()[:, 0]
     return [float(vals[r]) for r in regs]
 

@@ -52,9 +52,11 @@ def _failed(status):
     at a steady state: that transient is reported) and 5 (the same, its tight
     re-integration failed: the first pass's transient) are results, as the
     reference's find_steady returns wherever least_squares stops
-    (System._check with degenerate_ok); 1-3 are integrator failures."""
+    (System._check with degenerate_ok), and so is 6 (a DRC whose 2R+1
+    solves mix reached roots and transient ends: its xi are written, and
+    System.degree_of_rate_control warns); 1-3 are integrator failures."""
     st = np.asarray(status)
-    return np.nonzero((st != 0) & (st != 4) & (st != 5))[0]
+    return np.nonzero((st != 0) & (st != 4) & (st != 5) & (st != 6))[0]
 
 
 def _finals(sim_system, plan, ydyn, n):

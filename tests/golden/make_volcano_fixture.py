@@ -89,11 +89,16 @@ def _point(arg):
     where both exceed it has ok = False (reference transient) or tight_ok =
     False (tight transient) and is not compared on it.  With `reuse` (the
     stored y_ref, y_tight) only the derived columns are recomputed."""
-    from oracle import mk_oracle as O
     (i, j), reuse = arg
     be = np.linspace(-2.5, 0.5, G)
+    return (i, j) + (point_at(be[i], be[j], reuse),)
+
+
+def point_at(eco, eo, reuse=None):
+    """The oracle columns at one (E_CO, E_O) point (see _point)."""
+    from oracle import mk_oracle as O
     spec = copy.deepcopy(_spec)
-    O.set_volcano_point(spec, be[i], be[j])
+    O.set_volcano_point(spec, eco, eo)
 
     class Counted(O.ClassicModel):
         budget = None
@@ -152,12 +157,12 @@ def _point(arg):
         out['y_tight'], out['l10_tight'] = nan, np.nan
         out['regular'], out['newton_ok'], out['crit'] = False, False, np.inf
         out['y_root'], out['l10_root'] = nan, np.nan
-        return i, j, out
+        return out
     out['y_tight'], out['l10_tight'] = yT[dyn], l10(yT)
     yR = m.find_steady(yT.copy(), dist=ROOT_DIST, dist_atol=STEADY_ATOL)
     out['regular'], out['newton_ok'], out['crit'] = bool(m.regular), bool(m.newton_ok), float(m.root_crit)
     out['y_root'], out['l10_root'] = yR[dyn], l10(yR)
-    return i, j, out
+    return out
 
 
 def pick_points(corner_cells=None):

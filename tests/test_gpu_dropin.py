@@ -339,10 +339,13 @@ def test_drc_at_a_not_reached_node(P, inputs):
     """degree_of_rate_control(ss_solve=True) at a node whose transient has not
     reached a steady state returns its xi, as the reference's does (it never
     raises on least_squares' answer): every one of the 2R+1 solves reports by
-    the steady rule, and the batch's status says 4."""
+    the steady rule, and the batch's status says 4, or 6 where
+    some of the perturbed solves reach a root and others do not (ADVICE r4:
+    PCK_ST_DRC_MIXED, the central difference then mixes the rule's two
+    answers)."""
     s, eco, eo = _not_reached_node(P, inputs)
     d = s.drc_batch(('CO_ox',), T=[600.0], desc={'ECO': [eco], 'EO': [eo]}, eps=1e-3, steady=True)
-    assert d['status'][0] == 4, d['status']
+    assert d['status'][0] in (4, 6), d['status']
     assert all(np.isfinite(d[name][0]) for name in s.reactions)
     assert np.isfinite(d['tof0'][0]) and d['tof0'][0] > 0
 

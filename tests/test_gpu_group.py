@@ -39,45 +39,118 @@ def _volcano(P, inputs):
     return s
 
 
+SPLIT_FIXTURE = os.path.join(HERE, 'golden', 'split_fixture.npz')
+
+
+def _counts(x):
+    return dict(zip(*[v.tolist() for v in np.unique(x, return_counts=True)]))
+
+
+def _vs_oracle(name, r, ids, fx, near):
+    """A one-line account of one side's classification against the oracle's
+    rule (status 0 = the root is the answer), or '' if it agrees."""
+    reg = fx['regular']
+    got0 = r['status'] == 0
+    wrong = (got0 != reg) & ~near
+    odd = ~np.isin(r['status'], (0, 4))
+    if not wrong.any() and not odd.any():
+        return ''
+    idx = np.flatnonzero(wrong | odd)
+    pairs = _counts(np.array(['%d/%s' % (s, 'reg' if g else 'nr') for s, g in zip(r['status'][idx], reg[idx])]))
+    ex = ['#%d (E_CO %.4f, E_O %.4f, oracle crit %.3g, status %d, steps %d)' % (
+        k, fx['ECO'][k], fx['EO'][k], fx['crit'][k], r['status'][k], r['nsteps'][k]) for k in idx[:6]]
+    return ('%s (plan id %d, group kernel %d): statuses %s; %d of %d points off the oracle rule '
+            '(status/oracle pairs %s), e.g. %s' % (name, ids[0], ids[1], _counts(r['status']), idx.size,
+                                                   r['status'].size, pairs, '; '.join(ex)))
+
+
 def test_group_solver_matches_lane_solver_on_volcano(P, inputs):
     """The volcano network forced onto the lane-group solver (PCK_PLAN_GROUP)
-    against the one-lane-per-condition runtime-plan solver."""
+    against the one-lane-per-condition runtime-plan solver, and each of them
+    against the oracle's steady-state rule on the same 1024 points
+    (tests/golden/split_fixture.npz, make_split_fixture.py): a point may be
+    classified differently only where the oracle's criterion lies within 2x of
+    ROOT_DIST (none of these 1024 does; the nearest is 2.35x away).  A failure
+    names the side that is off, its status / oracle pairs and whether an
+    immediate repeat of that side gives bitwise the same statuses."""
+    from pycatkin_amd.classes.system import ROOT_DIST
+    fx = np.load(SPLIT_FIXTURE)
     s = _volcano(P, inputs)
     net = s.device(('CO_ox',))
     rng = np.random.default_rng(11)
     n = 1024
     kw = dict(T=np.full(n, 600.0), desc={'ECO': rng.uniform(-2.5, 0.5, n), 'EO': rng.uniform(-2.5, 0.5, n)},
               tof_terms=('CO_ox',), steady=True, activity=True)
-    net.set_plan_mode(1)
-    a = s.solve_batch(**kw)
-    net.set_plan_mode(2)
-    b = s.solve_batch(**kw)
-    net.set_plan_mode(0)
-    assert np.all((b['status'] == 0) | (b['status'] == 4)), np.unique(b['status'])
-    assert np.mean(a['status'] != b['status']) < 0.05
+    assert np.array_equal(kw['desc']['ECO'], fx['ECO']) and np.array_equal(kw['desc']['EO'], fx['EO'])
+    crit = fx['crit']
+    with np.errstate(divide='ignore', invalid='ignore'):
+        near = np.isfinite(crit) & (np.abs(np.log(crit / ROOT_DIST)) <= np.log(2.0))
+
+    def run(mode):
+        net.set_plan_mode(mode)
+        try:
+            r = s.solve_batch(**kw)
+            return r, (net.plan_id(), net.group_kernel())
+        finally:
+            net.set_plan_mode(0)
+
+    a, ida = run(1)
+    b, idb = run(2)
+    msgs = []
+    for name, mode, (r, ids) in (('lane runtime plan', 1, (a, ida)), ('lane group', 2, (b, idb))):
+        m = _vs_oracle(name, r, ids, fx, near)
+        if m:
+            r2, _ = run(mode)
+            m += '; a repeat of this side gives %s statuses (%d differ)' % (
+                'the same' if np.array_equal(r2['status'], r['status']) else 'different',
+                int((r2['status'] != r['status']).sum()))
+            msgs.append(m)
+    assert not msgs, ' || '.join(msgs)
     ok = (a['status'] == 0) & (b['status'] == 0)
-    assert ok.sum() > 0.8 * n
     same = np.isclose(b['tof'], a['tof'], rtol=1e-9, atol=0.0) | (b['tof'] == a['tof'])
     bad = ok & ~same
-    if os.path.isdir('gpurun_out'):
-        json.dump(dict(idx=np.flatnonzero(bad).tolist(), st=[a['status'][bad].tolist(), b['status'][bad].tolist()],
-                       act=[a['tof'][bad].tolist(), b['tof'][bad].tolist()],
-                       y_lane=a['y'][:, bad].T.tolist(), y_grp=b['y'][:, bad].T.tolist(),
-                       ECO=kw['desc']['ECO'][bad].tolist(), EO=kw['desc']['EO'][bad].tolist()),
-                  open('gpurun_out/diag_group_volcano.json', 'w'))
-    # bistable points whose transient has not settled at t_end may polish to a
-    # different root under different rounding; everything else agrees
-    assert bad.sum() <= max(2, 0.005 * ok.sum()), np.flatnonzero(bad)
+    assert bad.sum() <= max(2, 0.005 * ok.sum()), [(int(k), a['tof'][k], b['tof'][k]) for k in np.flatnonzero(bad)[:8]]
     np.testing.assert_allclose(b['y'][:, ok & same], a['y'][:, ok & same], rtol=1e-8, atol=1e-15)
     # transient only (no polish): same integrator, same steps up to rounding
     kw['steady'] = False
-    net.set_plan_mode(1)
-    a = s.solve_batch(**kw)
-    net.set_plan_mode(2)
-    b = s.solve_batch(**kw)
-    net.set_plan_mode(0)
-    assert np.all(b['status'] == 0)
+    a, ida = run(1)
+    b, idb = run(2)
+    assert np.all(a['status'] == 0) and np.all(b['status'] == 0), (ida, _counts(a['status']), idb, _counts(b['status']))
     np.testing.assert_allclose(b['tof'], a['tof'], rtol=1e-6)
+
+
+def test_group_drift_removal_keeps_species_outside_the_laws(P, inputs):
+    """The group integrator removes the stage increments' conserved-total
+    drift along y restricted to each law's own species (mk_group.h: kproj).
+    On the COOxReactor Pd111 CSTR the gas species (CO, O2, CO2) are dynamic
+    and outside the site balance: forced onto the lane-group solver, every
+    species of the transient and of the steady state matches the lane solver
+    (which has no drift removal), and the site total stays at its start."""
+    s = P.read_from_input_file(os.path.join(inputs, 'COOxReactor', 'input_Pd111.json'))
+    plan = s.plan(('CO_ox',))
+    net = s.device(('CO_ox',))
+    C = np.asarray(plan.conservation, float)
+    assert C.shape[0] >= 1
+    outside = np.all(C == 0.0, axis=0)
+    assert outside.any(), (plan.dyn, C)        # species outside every law exist
+    T = np.linspace(423.0, 623.0, 256)
+    for steady in (False, True):
+        kw = dict(T=T, tof_terms=('CO_ox',), steady=steady, rtol=1e-9, atol=1e-14)
+        a = s.solve_batch(**kw)
+        net.set_plan_mode(2)
+        try:
+            b = s.solve_batch(**kw)
+            gk = net.group_kernel()
+        finally:
+            net.set_plan_mode(0)
+        assert np.all(a['status'] == 0) and np.all(b['status'] == 0), (steady, _counts(a['status']), _counts(b['status']))
+        y0 = np.asarray(plan.y0_default, float)
+        np.testing.assert_allclose(C @ b['y'], np.repeat((C @ y0)[:, None], T.size, 1), rtol=1e-12, atol=1e-15,
+                                   err_msg='site totals, group kernel %d' % gk)
+        tol = 1e-7 if steady else 1e-6
+        assert close(b['y'][outside], a['y'][outside], rtol=tol, floor=1e-14), \
+            ('gas species', steady, np.max(np.abs(b['y'][outside] - a['y'][outside]) / np.abs(a['y'][outside])))
+        assert close(b['y'], a['y'], rtol=tol, floor=1e-14), ('all species', steady, gk)
 
 
 def test_group_rates_jacobian_on_volcano(P, inputs):

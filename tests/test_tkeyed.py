@@ -57,3 +57,44 @@ def test_tkeyed_batch_matches_per_temperature_constants():
         np.testing.assert_allclose(a['tof'][k], b['tof'][0], rtol=1e-10)
     # the barrier really enters: the TOFs differ across temperatures
     assert np.unique(np.round(np.log10(np.abs(a['tof'])), 6)).size == len(TS)
+
+
+def _tkeyed_reaction():
+    from pycatkin_amd.classes.reaction import UserDefinedReaction
+    return UserDefinedReaction(reac_type='Arrhenius', reversible=True, reactants=[], products=[], name='r',
+                               dErxn_user=dict(zip(TS, [-0.3, -0.32, -0.35, -0.31, -0.29])),
+                               dEa_fwd_user=dict(zip(TS, VALS)))
+
+
+def test_tkeyed_reaction_energy_forms_fill_from_T():
+    """get_reaction_energy / get_reaction_barriers compile the reaction's
+    energy forms and evaluate them for one condition: a T-keyed energy's
+    descriptor is filled from the table at that T (host side, no device
+    call), and a T the table lacks raises KeyError (reference dErxn_user[T])."""
+    from pycatkin_amd.engine import descriptor_values
+    from pycatkin_amd.network import compile_forms
+    r = _tkeyed_reaction()
+    e = r.energy_forms()
+    forms = [e['dErxn'], e['dEa_fwd'], e['dEa_rev']]
+    _, _, _, dnames = compile_forms(forms, {})
+    assert len(dnames) == 2 and all(k.startswith('@T:') for k in dnames)
+    v = descriptor_values(dnames, 600.0)
+    assert sorted(v.tolist()) == sorted([-0.35, 0.79])
+    with pytest.raises(KeyError):
+        descriptor_values(dnames, 610.0)
+    with pytest.raises(ValueError):
+        descriptor_values(dnames + ['ECO'], 600.0)
+
+
+@pytest.mark.gpu
+def test_tkeyed_reaction_getters_on_device():
+    """Reaction.get_reaction_energy / get_reaction_barriers with dict user
+    energies (reaction.py:71-83 of the drop-in; the reference reads
+    dErxn_user[T]) give the table's values at T, in J/mol."""
+    r = _tkeyed_reaction()
+    for T, v, dE in zip(TS, VALS, [-0.3, -0.32, -0.35, -0.31, -0.29]):
+        np.testing.assert_allclose(r.get_reaction_energy(T, 1e5, etype='electronic'), dE * 96.485e3, rtol=1e-12)
+        fwd, rev = r.get_reaction_barriers(T, 1e5, etype='electronic')
+        np.testing.assert_allclose([fwd, rev], [v * 96.485e3, (v - dE) * 96.485e3], rtol=1e-12)
+    with pytest.raises(KeyError):
+        r.get_reaction_energy(610.0, 1e5)

@@ -150,7 +150,9 @@ def rodas4(f, J, y, t0, t_end, rtol, atol, cons=None, max_steps=200000, cons_row
                 else:
                     for crow in np.asarray(cons, float):
                         if np.all(crow >= 0.0) and crow @ y > 0.0:
-                            k = k - y * ((crow @ k) / (crow @ y))
+                            # along the law's own species only: a species outside
+                            # it (a CSTR gas, another site type) keeps its stage
+                            k = k - np.where(crow != 0.0, y, 0.0) * ((crow @ k) / (crow @ y))
             ks.append(k)
             if i < 4:
                 u = y + sum(A[i + 1][j] * ks[j] for j in range(i + 1))

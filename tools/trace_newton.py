@@ -34,6 +34,10 @@ def main():
     lib = L.load()
     lib.pck_trace_set.argtypes = [C.c_longlong]
     lib.pck_trace_get.argtypes = [C.c_void_p, C.POINTER(C.c_int)]
+    split = '--split' in args          # K index the split fixture (tests/golden/split_fixture.npz) instead
+    if split:
+        args.remove('--split')
+        sf = np.load(os.path.join(ROOT, 'tests', 'golden', 'split_fixture.npz'))
     fx = dict(np.load(os.path.join(ROOT, 'tests', 'golden', 'volcano_fixture.npz')))
     lo, hi, G = fx['grid']
     be = np.linspace(lo, hi, int(G))
@@ -42,8 +46,11 @@ def main():
     plan = s.plan(('CO_ox',))
     out = {'dyn': list(plan.dyn)}
     for k in (int(a) for a in args):
-        kw = dict(T=np.full(1, 600.0), desc={'ECO': be[fx['i'][k:k + 1]], 'EO': be[fx['j'][k:k + 1]]},
-                  tof_terms=('CO_ox',))
+        if split:
+            desc = {'ECO': sf['ECO'][k:k + 1], 'EO': sf['EO'][k:k + 1]}
+        else:
+            desc = {'ECO': be[fx['i'][k:k + 1]], 'EO': be[fx['j'][k:k + 1]]}
+        kw = dict(T=np.full(1, 600.0), desc=desc, tof_terms=('CO_ox',))
         a = s.solve_batch(steady=False, rtol=STEADY_TRANSIENT[0], atol=STEADY_TRANSIENT[1], **kw)
         L.check(lib.pck_trace_set(0))
         d = s.solve_batch(steady=True, retry=None, y0=a['y'], t0=0.0, t_end=0.0, **kw)
