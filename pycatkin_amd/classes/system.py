@@ -450,8 +450,11 @@ class System:
         t_out, also the dynamic state at those times ('traj' [n_out, NS, n],
         RODAS4P dense output).
 
-        steady=True: the transient runs at STEADY_TRANSIENT unless rtol / atol
-        are given, and the Newton root of its end state is reported (status
+        steady=True: the transient runs at STEADY_TRANSIENT (1e-6 / 1e-22)
+        unless rtol / atol are given here -- the System's params['rtol'] /
+        ['atol'] (the input file's) are NOT used for steady solves, since the
+        rule's distance test needs relative error control on every coverage
+         -- and the Newton root of its end state is reported (status
         0) where the transient has reached it to `root_dist` ('auto':
         ROOT_DIST when t_end > t0, else 0 -- a polish of the given state, as
         find_steady); elsewhere the transient end (status 4).  `retry` =
