@@ -309,7 +309,7 @@ def _outputs(torch, net, n, L, _ptr):
 def _solve_workload(wl, sim, net, plan, n, T, p, desc, tof_terms, steady, activity, t_end=None, rtol=None,
                     atol=None, args=None):
     import torch
-    from pycatkin_amd.classes.system import ROOT_DIST, STEADY_TRANSIENT
+    from pycatkin_amd.classes.system import ROOT_DIST, SCREEN_MARGIN, SCREEN_RTOL, STEADY_TRANSIENT
     from pycatkin_amd import _lib as L
     from pycatkin_amd.engine import _ptr
     Tt, pp, d, fx, y0, inflow = sim._inputs(net, plan, n, T, p, desc, None, None, None)
@@ -327,12 +327,17 @@ def _solve_workload(wl, sim, net, plan, n, T, p, desc, tof_terms, steady, activi
                         newton=steady and not args.no_newton, newton_iters=60, activity=activity,
                         retry=tuple(args.retry) if args.retry else None,
                         root_dist=(ROOT_DIST if args.root_dist is None else args.root_dist) if steady else 0.0)
+    # the screening pass of System.solve_batch(steady=True) (SCREEN_RTOL; --screen 0: off)
+    scr = SCREEN_RTOL if getattr(args, 'screen', None) is None else args.screen
+    if steady and wl.prm.newton and wl.prm.root_dist > 0.0 and not args.retry and scr > 0.0:
+        wl.prm.screen_rtol, wl.prm.screen_margin = float(scr), SCREEN_MARGIN
     wl.tolerances = (wl.prm.rtol, wl.prm.atol)
     wl.prm.wave_order = {'auto': 0, 'on': 1, 'off': -1}[getattr(args, 'wave_order', 'auto')]
     # solver launches per step: the first pass, the degenerate-root retry and,
     # on the lane solver with cost-ordered dispatch, its preview
     ordered = net.NDYN <= 8 and (wl.prm.wave_order == 1 or (wl.prm.wave_order == 0 and n >= 262144))
-    wl.solver_launches = 1 + int(bool(wl.prm.newton and wl.prm.retry_rtol > 0.0)) + int(ordered)
+    screened = net.NDYN <= 8 and wl.prm.screen_rtol > 0.0
+    wl.solver_launches = 1 + int(bool(wl.prm.newton and wl.prm.retry_rtol > 0.0)) + int(ordered) + int(screened)
     wl.out, wl.o = _outputs(torch, net, n, L, _ptr)
     wl.kf = torch.empty((max(net.NRXN, 1), max(n, 1)), dtype=torch.float64, device='cuda')
     wl.kr = torch.empty_like(wl.kf)
@@ -385,13 +390,19 @@ def volcano_workload(args, rank, world):
                     ('CO_ox',), True, True, args=args)
     # the profile tag names the per-GPU workload: a weak-scaling rank's share is
     # the same 1024 x 1024 solve at every N, so N > 1 lines carry its counters
-    wl.tag = 'volcano %dx%d %s rtol %g atol %g' % (rows, G, args.order, wl.prm.rtol, wl.prm.atol)
+    wl.tag = 'volcano %dx%d %s rtol %g atol %g' % (rows, G, args.order, wl.prm.rtol, wl.prm.atol) + \
+        (' screen %g' % wl.prm.screen_rtol if wl.prm.screen_rtol > 0.0 else '')
     wl.config = {'workload': 'COOxVolcano %dx%d (E_CO x E_O) grid, %s over %d GPU(s): %d E_CO rows x %d E_O per rank, '
                              'T=600 K, transient to t_end=3600 s at rtol %g / atol %g, Newton steady-state polish, '
-                             'the root where the transient has reached it to %g (else the transient end), activity'
+                             'the root where the transient has reached it to %g (else the transient end), activity%s'
                              % (wl.global_grid[0], wl.global_grid[1], 'sharded' if args.scaling == 'strong'
                                 else 'one grid share per GPU', world, rows, G, wl.prm.rtol, wl.prm.atol,
-                                wl.prm.root_dist),
+                                wl.prm.root_dist,
+                                '; screening pass at rtol %g accepting roots within %g of its transient end, the '
+                                'rest solved again at rtol %g' % (wl.prm.screen_rtol,
+                                                                  wl.prm.screen_margin * wl.prm.root_dist,
+                                                                  wl.prm.rtol)
+                                if wl.prm.screen_rtol > 0.0 else ''),
                  'global_grid': list(wl.global_grid), 'grid_per_gpu': [rows, G],
                  'parallelism': 'dp%d' % world, 'shard': 'cyclic E_CO rows',
                  'order': 'row' if wl.perm is None else 'tile %s' % args.tile}
@@ -568,6 +579,8 @@ def build_parser():
     ap.add_argument('--atol', type=float, default=0.0, help='A/B: first-pass atol (0: the input\'s)')
     ap.add_argument('--retry', type=float, nargs=2, default=None, metavar=('RTOL', 'ATOL'),
                     help='A/B: integrate the status-4 conditions again at these tolerances (default: no retry)')
+    ap.add_argument('--screen', type=float, default=None,
+                    help='screening-pass rtol of steady solves (default SCREEN_RTOL; 0: off)')
     ap.add_argument('--root-dist', type=float, default=None,
                     help='A/B: pck_solve_params.root_dist of steady solves (default ROOT_DIST)')
     ap.add_argument('--emulate', default=None, metavar='R/N',
@@ -728,7 +741,7 @@ def main(argv=None):
                     'kernel': wl.kernel_name, 'kernel_ms': k3_ms, 'rate_constants_ms': k1_ms,
                     'flops_per_launch': fl, 'flops_structural': fl_struct, 'flops_pmc_f64': fl_pmc,
                     'flops_per_step': fps, 'flop_count': 'min(structural nonzeros of one accepted RODAS4P step x '
-                    'integrator steps of rank 0 (first pass + retry; the preview, Newton polish, kernel 1 and TOF not counted), '
+                    'integrator steps of rank 0 (every solver pass: screening + full, or first pass + retry; the preview, Newton polish, kernel 1 and TOF not counted), '
                     '64 x (ADD+MUL+TRANS) + 128 x FMA fp64 wave instructions of the committed PMC profile of this '
                     'workload, per launch x solver launches per step)',
                     'integrator_steps': steps_local, 'lane_efficiency': lane_eff, 'solver_launches_per_step': nl}

@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define PCK_ABI_VERSION 5
+#define PCK_ABI_VERSION 6
 
 /* error codes */
 #define PCK_OK 0
@@ -163,6 +163,17 @@ typedef struct {
                             *   PCK_ST_NEWTON (old_system.py:517-529 System.activity semantics).
                             *   0: any converged, balanced, non-negative root is reported
                             *   (old_system.py:385-468 find_steady from a given state). */
+    double screen_rtol;    /* with newton and root_dist > 0 (pck_solve on the one-lane path, no
+                            *   trajectory, no retry_rtol): a screening pass at rtol = screen_rtol
+                            *   (atol scaled alike) whose Newton root is accepted (PCK_ST_OK) only if
+                            *   the screening transient's end lies within screen_margin * root_dist
+                            *   of it; every other condition is then solved again from y0 at
+                            *   rtol / atol by a second launch over their compacted list, exactly
+                            *   as without screening (y, tof, status of that solve; nsteps adds the
+                            *   two passes).  A transient that has settled on a root ends on it
+                            *   at any tolerance, so the accepted conditions report the root the
+                            *   single pass would (DESIGN.md "Screening pass").  0: off. */
+    double screen_margin;  /*   fraction of root_dist for the screening pass's acceptance (0: 0.1) */
 } pck_solve_params;
 
 /* Outputs of pck_solve (device pointers; any may be NULL). */

@@ -18,7 +18,7 @@ EXPORTED = ('pck_abi_version', 'pck_last_error', 'pck_network_create', 'pck_netw
             'pck_network_dims', 'pck_network_set_plan_mode', 'pck_energies', 'pck_rate_constants', 'pck_species_rates',
             'pck_reaction_rates', 'pck_jacobian', 'pck_solve', 'pck_drc')
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 # header slot indices (must match the enums of include/pycatkin_amd.h)
 I_VERSION, I_NDESC, I_NTH, I_NREG, I_NRXN, I_NDYN, I_NFIX, I_NCONS, I_NTOF = range(9)
@@ -51,7 +51,7 @@ class SolveParams(C.Structure):
                 ('max_steps', C.c_int32), ('newton', C.c_int32), ('newton_iters', C.c_int32),
                 ('want_activity', C.c_int32), ('drc_eps', C.c_double), ('t_out', C.c_void_p), ('n_out', C.c_int64),
                 ('retry_rtol', C.c_double), ('retry_atol', C.c_double), ('wave_order', C.c_int32),
-                ('root_dist', C.c_double)]
+                ('root_dist', C.c_double), ('screen_rtol', C.c_double), ('screen_margin', C.c_double)]
 
 
 class Outputs(C.Structure):

@@ -40,6 +40,15 @@ STEADY_TRANSIENT = (1.0e-6, 1.0e-22)
 ROOT_DIST = 1.0e-6
 # round-3 name of the tight tolerances (the retry pass, now optional)
 DEGENERATE_RETRY = STEADY_TRANSIENT
+# Screening pass of steady solves (round 5, pck_solve_params.screen_rtol;
+# DESIGN.md "Screening pass"): the rule first at rtol SCREEN_RTOL (atol scaled
+# alike), a root accepted there only within SCREEN_MARGIN * ROOT_DIST of the
+# screening transient's end; every other condition is solved again at
+# STEADY_TRANSIENT exactly as without screening.  A transient that has settled
+# on its root ends on it at any tolerance, so the accepted conditions report
+# the same root.
+SCREEN_RTOL = 1.0e-3
+SCREEN_MARGIN = 0.1
 
 
 def _retry_tolerances(retry):
@@ -444,7 +453,7 @@ class System:
 
     def solve_batch(self, T=None, p=None, desc=None, y0=None, fix=None, inflow=None, tof_terms=(),
                     steady=False, activity=False, t_end=None, t0=None, rtol=None, atol=None, max_steps=200000,
-                    newton_iters=60, to_numpy=True, t_out=None, retry=None, root_dist='auto'):
+                    newton_iters=60, to_numpy=True, t_out=None, retry=None, root_dist='auto', screen='auto'):
         """Transient solve to t_end (solve_odes), optionally polished to the
         steady state (find_steady), with TOF or activity per condition; with
         t_out, also the dynamic state at those times ('traj' [n_out, NS, n],
@@ -459,7 +468,11 @@ class System:
         ROOT_DIST when t_end > t0, else 0 -- a polish of the given state, as
         find_steady); elsewhere the transient end (status 4).  `retry` =
         (rtol, atol) integrates the status-4 conditions again at those
-        tolerances in a second launch (None: no second pass)."""
+        tolerances in a second launch (None: no second pass).  `screen`
+        ('auto': SCREEN_RTOL for steady solves with root_dist > 0, no retry
+        and no t_out; None: off; a number: the screening rtol) runs the rule
+        at that loose tolerance first and solves only the conditions it does
+        not accept at the transient tolerances (one-lane networks)."""
         plan = self.plan(tuple(tof_terms), None)
         net = self.device(tuple(tof_terms), None)
         sizes = [T, p] + (list(desc.values()) if desc else [])
@@ -477,12 +490,17 @@ class System:
             if root_dist != 'auto':
                 raise ValueError("root_dist must be 'auto' or a number in [0, 1)")
             root_dist = ROOT_DIST if (steady and t_end > t0) else 0.0
+        if isinstance(screen, str):
+            if screen != 'auto':
+                raise ValueError("screen must be 'auto', None or an rtol")
+            screen = SCREEN_RTOL if (steady and root_dist > 0.0 and retry is None and t_out is None) else None
         out = net.solve(n, T, p, y0, d, fx, inflow, t0=t0, t_end=t_end,
                         rtol=self.params['rtol'] if rtol is None else rtol,
                         atol=self.params['atol'] if atol is None else atol,
                         max_steps=max_steps, newton=steady, newton_iters=newton_iters, activity=activity,
                         t_out=t_out, retry=_retry_tolerances(retry) if steady else None,
-                        root_dist=float(root_dist) if steady else 0.0)
+                        root_dist=float(root_dist) if steady else 0.0,
+                        screen=(float(screen), SCREEN_MARGIN) if (steady and screen) else None)
         if to_numpy:
             return {k: v.cpu().numpy() for k, v in out.items()}
         return out

@@ -185,6 +185,29 @@ __device__ __forceinline__ double rcp(double x) {
 #endif
 }
 
+// One Newton step on the v_rcp_f64 estimate: the estimate's relative error
+// is <= 4.6e-8, so one step leaves <= 2.3e-15 (two steps are correctly
+// rounded on all 2^24 inputs of tools/rcp_accuracy.hip, measured on gfx950).
+// 16 + 8 cycles instead of 16 + 16: for the lane integrator's step-size
+// reciprocal, its stage LU pivots and the site-balance projection, where a
+// few ulps only perturb the stage matrix or a scale factor by rounding
+// (PCK_LANE_FAST below).
+__device__ __forceinline__ double rcp1(double x) {
+    const double r = __builtin_amdgcn_rcp(x);
+    return fma(fma(-x, r, 1.0), r, r);
+}
+
+// Cheaper arithmetic in the one-lane integrator (mk_solver.h: integrate and
+// the threshold-pivoting lu): the pivot reciprocals, 1/h and the projection
+// factor from rcp1; the threshold rule's pivot search only where some lane of
+// the wavefront needs it (one max per row and one compare per column on the
+// common path); the stage right-hand sides with the 1/h-scaled coefficients
+// computed once per step; the step-size factor from v_log_f32 / v_exp_f32.
+// 0 = the round-4 arithmetic (A/B).  Results move by rounding only.
+#ifndef PCK_LANE_FAST
+#define PCK_LANE_FAST 1
+#endif
+
 // Double-double arithmetic (hi + lo, |lo| <= ulp(hi) / 2) for the Newton
 // refinement's residual (mk_solver.h: newton): error-free products by FMA
 // and Knuth's two-sum, so a balance of 1e11 / s fluxes that cancel to O(1)
@@ -239,6 +262,14 @@ __device__ __forceinline__ double step_factor(double q) {
     return 0.9 * (double)__builtin_amdgcn_rsqf(__builtin_amdgcn_sqrtf(__builtin_amdgcn_sqrtf(qf)));
 }
 
+// the same factor from two fp32 transcendentals, 0.9 * 2^(-log2(q) / 8)
+// (PCK_LANE_FAST: one fewer quarter-rate instruction on the controller's
+// dependent chain)
+__device__ __forceinline__ double step_factor_fast(double q) {
+    const float qf = (float)q;
+    return (double)(0.9f * __builtin_amdgcn_exp2f(-0.125f * __builtin_amdgcn_logf(qf)));
+}
+
 // In-register LU with threshold partial pivoting (row swaps by predicated
 // selects so every register index stays static).  The diagonal is kept
 // unless a row below is more than 1/PIVOT_TAU times larger (the classic
@@ -258,12 +289,68 @@ constexpr double PIVOT_TAU = PCK_PIVOT_TAU;
 // by the oracle (LAPACK partial pivoting) from the same start state
 // (tools/flip_probe.py).  The Rosenbrock matrices I/(h g) - J are
 // diagonally dominant enough for the threshold rule, which swaps rarely.
+template <int NS>
+__device__ __forceinline__ void lu_swap_rows(double (&A)[NS][NS], int k, int p) {
+    // the trailing columns only (LINPACK's dgefa): the multipliers of the
+    // earlier columns stay in the rows they were computed in, which is what
+    // lu_solve's forward sweep -- swap b[k], then eliminate with column k --
+    // assumes.  Rounds 1-4 swapped whole rows here (LAPACK's storage, whose
+    // solve applies every swap first), so a swap at column k >= 1 left the
+    // solve with a wrong L: 95 % of random 5 x 5 systems solved to O(1) error
+    // (DESIGN.md "LU").
+#pragma unroll
+    for (int r = k + 1; r < NS; ++r) {
+        const bool sw = (p == r);
+#pragma unroll
+        for (int q = k; q < NS; ++q) {
+            const double a = A[k][q], b = A[r][q];
+            A[k][q] = sw ? b : a;
+            A[r][q] = sw ? a : b;
+        }
+    }
+}
+
 template <int NS, bool PARTIAL = false>
 __device__ __forceinline__ bool lu(double (&A)[NS][NS], int (&piv)[NS], unsigned& swaps) {
     bool ok = true;
     swaps = 0u;
 #pragma unroll
     for (int k = 0; k < NS; ++k) {
+        if (PCK_LANE_FAST && !PARTIAL) {
+            // threshold rule, common path: the largest sub-diagonal entry of
+            // column k against |A[k][k]| / tau; the search for the pivot row
+            // runs only when some lane of the wavefront swaps (same pivots)
+            const double dk = fabs(A[k][k]) * (1.0 / PIVOT_TAU);
+            double m = 0.0;
+#pragma unroll
+            for (int r = k + 1; r < NS; ++r) m = fmax(m, fabs(A[r][k]));
+            piv[k] = k;
+            if (__any(m > dk)) {
+                int p = k;
+                double best = dk;
+#pragma unroll
+                for (int r = k + 1; r < NS; ++r) {
+                    const double a = fabs(A[r][k]);
+                    p = (a > best) ? r : p;
+                    best = fmax(best, a);
+                }
+                piv[k] = p;
+                swaps |= 1u << k;
+                lu_swap_rows(A, k, p);
+            }
+            const double d = A[k][k];
+            ok = ok && (d != 0.0) && (d == d);
+            const double inv = rcp1(d);
+#pragma unroll
+            for (int r = k + 1; r < NS; ++r) {
+                const double l = A[r][k] * inv;
+                A[r][k] = l;
+#pragma unroll
+                for (int q = k + 1; q < NS; ++q) A[r][q] -= l * A[k][q];
+            }
+            A[k][k] = inv;
+            continue;
+        }
         int p = k;
         double best = fabs(A[k][k]) * (PARTIAL ? 1.0 : 1.0 / PIVOT_TAU);   // a multiply, not an IEEE divide
 #pragma unroll
@@ -275,23 +362,7 @@ __device__ __forceinline__ bool lu(double (&A)[NS][NS], int (&piv)[NS], unsigned
         piv[k] = p;
         if (__any(p != k)) {
             swaps |= 1u << k;
-            // the trailing columns only (LINPACK's dgefa): the multipliers of
-            // the earlier columns stay in the rows they were computed in, which
-            // is what lu_solve's forward sweep -- swap b[k], then eliminate
-            // with column k -- assumes.  Rounds 1-4 swapped whole rows here
-            // (LAPACK's storage, whose solve applies every swap first), so a
-            // swap at column k >= 1 left the solve with a wrong L: 95 % of
-            // random 5 x 5 systems solved to O(1) error (DESIGN.md "LU").
-#pragma unroll
-            for (int r = k + 1; r < NS; ++r) {
-                const bool sw = (p == r);
-#pragma unroll
-                for (int q = k; q < NS; ++q) {
-                    const double a = A[k][q], b = A[r][q];
-                    A[k][q] = sw ? b : a;
-                    A[r][q] = sw ? a : b;
-                }
-            }
+            lu_swap_rows(A, k, p);
         }
         const double d = A[k][k];
         ok = ok && (d != 0.0) && (d == d);

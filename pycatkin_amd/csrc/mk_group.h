@@ -1719,6 +1719,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 64
     }
 }
 
+// (not in the kernel-only translation units of the split build, csrc/mk_inst.h:
+// a non-template kernel is defined once, with the C-ABI)
+#ifndef PCK_KERNEL_TU
 // DRC combine (old_system.py:490-515): xi_j = (TOF_j+ - TOF_j-) / (2 eps TOF_0)
 __global__ void __launch_bounds__(256) k_drc_combine(int64_t n, int R, double eps, const double* tofbuf,
                                                      const int32_t* stbuf, const int32_t* nsbuf, double* xi,
@@ -1743,6 +1746,7 @@ __global__ void __launch_bounds__(256) k_drc_combine(int64_t n, int R, double ep
     if (status) status[c] = st;
     if (nsteps) nsteps[c] = ns;
 }
+#endif  // PCK_KERNEL_TU
 
 template <int NSP, int G, int P>
 __global__ void __launch_bounds__(64) k_rates_grp(NetView nv, GrpView gv, CondView cv, const double* kf,

@@ -114,6 +114,26 @@ __global__ void __launch_bounds__(64) k_energies(NetView nv, CondView cv, double
 
 #include "mk_solver.h"
 
+// The solver kernels are compiled in translation units of their own in the
+// product build (csrc/mk_inst.h, csrc/tu_*.hip): here they are only declared.
+#ifndef PCK_SPLIT_TU
+#define PCK_SPLIT_TU 0
+#endif
+#if PCK_SPLIT_TU
+#include "mk_inst.h"
+namespace pck {
+#define PCK_X(N) PCK_DO_LANE_RT(extern, N)
+PCK_INST_LANE_RT(PCK_X)
+#undef PCK_X
+#define PCK_X(id, T) PCK_DO_LANE_CT(extern, id, T)
+PCK_COMPILED_NETWORKS(PCK_X)
+#undef PCK_X
+#define PCK_X(NP, GG, PP) PCK_DO_GRP(extern, NP, GG, PP)
+PCK_INST_GRP(PCK_X)
+#undef PCK_X
+}  // namespace pck
+#endif
+
 // forward / reverse rate of every active reaction at states y, fixed species
 // folded in (System._calc_rates, system.py:345-376; old_system.py:202-225
 // reaction_terms).  One lane per condition; not on the solve path.
@@ -736,6 +756,10 @@ static int check_params(const pck_solve_params* prm) {
     if (!(prm->root_dist >= 0.0 && prm->root_dist < 1.0)) return fail(PCK_E_ARG, "root_dist must be in [0, 1)%s", "");
     if (prm->retry_rtol != 0.0 && !(prm->retry_rtol > 0.0 && prm->retry_atol > 0.0))
         return fail(PCK_E_ARG, "retry tolerances must both be positive (or retry_rtol 0)%s", "");
+    if (!(prm->screen_rtol >= 0.0) || !(prm->screen_margin >= 0.0 && prm->screen_margin <= 1.0))
+        return fail(PCK_E_ARG, "screen_rtol must be >= 0 and screen_margin in [0, 1]%s", "");
+    if (prm->screen_rtol > 0.0 && prm->retry_rtol > 0.0)
+        return fail(PCK_E_ARG, "screen_rtol and retry_rtol are exclusive%s", "");
     return PCK_OK;
 }
 
@@ -745,10 +769,11 @@ static int check_params(const pck_solve_params* prm) {
 // The list's order across wavefronts follows the atomics; every lane's solve
 // is independent of which lanes share its wavefront, so results do not
 // depend on it.
+// want < 0: every status but PCK_ST_OK (the screening pass's rejects)
 __global__ void __launch_bounds__(256) k_select_status(int64_t n, const int32_t* status, int32_t want,
                                                        int64_t* idx, int32_t* cnt) {
     const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const bool f = (c < n) && status[c] == want;
+    const bool f = (c < n) && (want < 0 ? status[c] != PCK_ST_OK : status[c] == want);
     const unsigned long long m = __ballot(f);
     if (m == 0ull) return;                             // wave-uniform
     const int lane = threadIdx.x & 63;
@@ -1018,6 +1043,11 @@ static int launch_solve(const pck_network* net, const pck_conditions* cond, cons
     // their compacted list (pck_solve only: G == 1, no DRC groups)
     bool retry = prm->newton && prm->retry_rtol > 0.0 && !drc_groups && a.G == 1;
     const bool traj = (prm->n_out > 0 && a.traj != nullptr);
+    // screening pass (pck_solve_params.screen_rtol): the steady rule at a
+    // loose tolerance with a tighter acceptance, then the single pass at the
+    // caller's tolerances over the rest (one-lane path, pck_solve only)
+    bool screen = prm->newton && prm->root_dist > 0.0 && prm->screen_rtol > 0.0 && prm->screen_rtol > prm->rtol &&
+                  !drc_groups && a.G == 1 && !traj;
     if (traj) {
         if (!prm->t_out) return fail(PCK_E_ARG, "n_out > 0 without t_out%s", "");
         if (drc_groups || a.G != 1) return fail(PCK_E_ARG, "trajectory output is for pck_solve only%s", "");
@@ -1034,6 +1064,7 @@ static int launch_solve(const pck_network* net, const pck_conditions* cond, cons
         a.cons_rows = (e && e[0] == '1');
     }
     const bool grp = drc_groups || use_group(net, a.G);
+    screen = screen && !grp;
     if (grp && !net->grp_ok)
         return fail(PCK_E_SIZE, "lane-group solver: a reaction has more than 6 dynamic participants%s", "");
     GrpArgs ga;
@@ -1097,7 +1128,7 @@ static int launch_solve(const pck_network* net, const pck_conditions* cond, cons
         a.worder = wo;
     }
     StreamScratch rscr;
-    if (retry) {
+    if (retry || screen) {
         // the retry list (int64 per condition), its length, and a status
         // array when the caller passed none
         // (W wavefronts' worth of entries: the overlapped split keeps two lists)
@@ -1154,6 +1185,29 @@ static int launch_solve(const pck_network* net, const pck_conditions* cond, cons
         if (rc) return rc;
         HIPCHK(hipStreamWaitEvent(s, ss->done, 0));        // the caller's stream sees both retries
         retry = false;                                     // done
+    } else if (screen) {
+        // pass 1: the steady rule at screen_rtol (atol scaled alike), a root
+        // accepted only within screen_margin * root_dist of the transient end
+        SolveArgs a1 = a;
+        a1.rtol = prm->screen_rtol;
+        a1.atol = a.atol * (prm->screen_rtol / a.rtol);
+        a1.root_dist = a.root_dist * (prm->screen_margin > 0.0 ? prm->screen_margin : 0.1);
+        rc = run_solver(net, cond, a1, grp, ga, traj, kf, kr, s);
+        if (rc) return rc;
+        // pass 2: every other condition, from y0 at the caller's tolerances
+        int64_t* idx = rscr.as<int64_t>();
+        int32_t* cnt = (int32_t*)(idx + ((n + PCK_SOLVE_BLOCK - 1) / PCK_SOLVE_BLOCK) * PCK_SOLVE_BLOCK);
+        HIPCHK(hipMemsetAsync(cnt, 0, sizeof(int32_t), s));
+        hipLaunchKernelGGL(k_select_status, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, a.status, -1,
+                           idx, cnt);
+        HIPCHK(hipGetLastError());
+        SolveArgs a2 = a;
+        a2.idx = idx;
+        a2.nidx = cnt;
+        a2.retry_pass = 2;
+        a2.worder = nullptr;
+        rc = run_solver(net, cond, a2, grp, ga, false, kf, kr, s);
+        if (rc) return rc;
     } else {
         rc = run_solver(net, cond, a, grp, ga, traj, kf, kr, s);
         if (rc) return rc;

@@ -558,7 +558,7 @@ __device__ PCK_LANE_INLINE int integrate(const P& p, const Lane<P::NS>& L, const
         if (t + h >= t_end) { h = t_end - t; last = true; }
         double ih, ig;
         PCK_LPH(0, jac(p, L, k, y, W);                               // W = I/(h g) - J
-               ih = rcp(h); ig = ih * (1.0 / g);
+               ih = PCK_LANE_FAST ? rcp1(h) : rcp(h); ig = ih * (1.0 / g);
                for (int i = 0; i < NS; ++i) {
                    for (int q = 0; q < NS; ++q) W[i][q] = -W[i][q];
                    W[i][i] += ig;
@@ -572,28 +572,44 @@ __device__ PCK_LANE_INLINE int integrate(const P& p, const Lane<P::NS>& L, const
             continue;
         }
         double k1[NS], k2[NS], k3[NS], k4[NS], k5[NS], u[NS], fu[NS];
+        // the stage coefficients C_ij / h, once per step (PCK_LANE_FAST): every
+        // stage right-hand side is then a chain of FMAs on f(u_i)
+        const double h21 = PCK_LANE_FAST ? ih * C21 : 0.0, h31 = PCK_LANE_FAST ? ih * C31 : 0.0,
+                     h32 = PCK_LANE_FAST ? ih * C32 : 0.0, h41 = PCK_LANE_FAST ? ih * C41 : 0.0,
+                     h42 = PCK_LANE_FAST ? ih * C42 : 0.0, h43 = PCK_LANE_FAST ? ih * C43 : 0.0,
+                     h51 = PCK_LANE_FAST ? ih * C51 : 0.0, h52 = PCK_LANE_FAST ? ih * C52 : 0.0,
+                     h53 = PCK_LANE_FAST ? ih * C53 : 0.0, h54 = PCK_LANE_FAST ? ih * C54 : 0.0,
+                     h61 = PCK_LANE_FAST ? ih * C61 : 0.0, h62 = PCK_LANE_FAST ? ih * C62 : 0.0,
+                     h63 = PCK_LANE_FAST ? ih * C63 : 0.0, h64 = PCK_LANE_FAST ? ih * C64 : 0.0,
+                     h65 = PCK_LANE_FAST ? ih * C65 : 0.0;
 #pragma unroll
         for (int i = 0; i < NS; ++i) k1[i] = F0[i];
         if (PCK_CONS_ROWS && crows) cons_zero(p, k1);
         PCK_LPH(2, lu_solve<NS>(W, piv, sw, k1));
         PCK_LPH(4, for (int i = 0; i < NS; ++i) u[i] = y[i] + a21 * k1[i]);
         PCK_LPH(3, rhs(p, L, k, u, fu));
-        PCK_LPH(4, for (int i = 0; i < NS; ++i) k2[i] = fu[i] + ih * (C21 * k1[i]));
+        PCK_LPH(4, for (int i = 0; i < NS; ++i)
+                       k2[i] = PCK_LANE_FAST ? fu[i] + h21 * k1[i] : fu[i] + ih * (C21 * k1[i]));
         if (PCK_CONS_ROWS && crows) cons_zero(p, k2);
         PCK_LPH(2, lu_solve<NS>(W, piv, sw, k2));
         PCK_LPH(4, for (int i = 0; i < NS; ++i) u[i] = y[i] + a31 * k1[i] + a32 * k2[i]);
         PCK_LPH(3, rhs(p, L, k, u, fu));
-        PCK_LPH(4, for (int i = 0; i < NS; ++i) k3[i] = fu[i] + ih * (C31 * k1[i] + C32 * k2[i]));
+        PCK_LPH(4, for (int i = 0; i < NS; ++i)
+                       k3[i] = PCK_LANE_FAST ? fu[i] + h31 * k1[i] + h32 * k2[i] : fu[i] + ih * (C31 * k1[i] + C32 * k2[i]));
         if (PCK_CONS_ROWS && crows) cons_zero(p, k3);
         PCK_LPH(2, lu_solve<NS>(W, piv, sw, k3));
         PCK_LPH(4, for (int i = 0; i < NS; ++i) u[i] = y[i] + a41 * k1[i] + a42 * k2[i] + a43 * k3[i]);
         PCK_LPH(3, rhs(p, L, k, u, fu));
-        PCK_LPH(4, for (int i = 0; i < NS; ++i) k4[i] = fu[i] + ih * (C41 * k1[i] + C42 * k2[i] + C43 * k3[i]));
+        PCK_LPH(4, for (int i = 0; i < NS; ++i)
+                       k4[i] = PCK_LANE_FAST ? fu[i] + h41 * k1[i] + h42 * k2[i] + h43 * k3[i]
+                                             : fu[i] + ih * (C41 * k1[i] + C42 * k2[i] + C43 * k3[i]));
         if (PCK_CONS_ROWS && crows) cons_zero(p, k4);
         PCK_LPH(2, lu_solve<NS>(W, piv, sw, k4));
         PCK_LPH(4, for (int i = 0; i < NS; ++i) u[i] = y[i] + a51 * k1[i] + a52 * k2[i] + a53 * k3[i] + a54 * k4[i]);
         PCK_LPH(3, rhs(p, L, k, u, fu));
-        PCK_LPH(4, for (int i = 0; i < NS; ++i) k5[i] = fu[i] + ih * (C51 * k1[i] + C52 * k2[i] + C53 * k3[i] + C54 * k4[i]));
+        PCK_LPH(4, for (int i = 0; i < NS; ++i)
+                       k5[i] = PCK_LANE_FAST ? fu[i] + h51 * k1[i] + h52 * k2[i] + h53 * k3[i] + h54 * k4[i]
+                                             : fu[i] + ih * (C51 * k1[i] + C52 * k2[i] + C53 * k3[i] + C54 * k4[i]));
         if (PCK_CONS_ROWS && crows) cons_zero(p, k5);
         PCK_LPH(2, lu_solve<NS>(W, piv, sw, k5));
         double d2[TRAJ ? NS : 1], d3[TRAJ ? NS : 1];
@@ -609,7 +625,9 @@ __device__ PCK_LANE_INLINE int integrate(const P& p, const Lane<P::NS>& L, const
         PCK_LPH(3, rhs(p, L, k, u, fu));
         // k6 reuses k5's registers once k5 is folded into u
         PCK_LPH(4, for (int i = 0; i < NS; ++i)
-                       k5[i] = fu[i] + ih * (C61 * k1[i] + C62 * k2[i] + C63 * k3[i] + C64 * k4[i] + C65 * k5[i]));
+                       k5[i] = PCK_LANE_FAST
+                                   ? fu[i] + h61 * k1[i] + h62 * k2[i] + h63 * k3[i] + h64 * k4[i] + h65 * k5[i]
+                                   : fu[i] + ih * (C61 * k1[i] + C62 * k2[i] + C63 * k3[i] + C64 * k4[i] + C65 * k5[i]));
         if (PCK_CONS_ROWS && crows) cons_zero(p, k5);
         PCK_LPH(2, lu_solve<NS>(W, piv, sw, k5));
         PCK_LPH_MARK();
@@ -631,7 +649,7 @@ __device__ PCK_LANE_INLINE int integrate(const P& p, const Lane<P::NS>& L, const
         // drives a component below -atol is rejected and retried at the
         // fraction of the step where that component reaches -atol
         const bool negv = PCK_POSITIVITY && umin < -atol;
-        const double fac = step_factor(q);
+        const double fac = PCK_LANE_FAST ? step_factor_fast(q) : step_factor(q);
         if (q <= 1.0 && !negv) {
             const double t_old = t;
             t = last ? t_end : t + h;
@@ -654,7 +672,7 @@ __device__ PCK_LANE_INLINE int integrate(const P& p, const Lane<P::NS>& L, const
                     sm += p.C(l, i) * y[i];
                 }
                 if (pos && sm > 0.0) {
-                    const double fct = cons0[l] * rcp(sm);
+                    const double fct = cons0[l] * (PCK_LANE_FAST ? rcp1(sm) : rcp(sm));
 #pragma unroll
                     for (int i = 0; i < NS; ++i)
                         if (p.C(l, i) != 0.0) y[i] *= fct;
@@ -1224,6 +1242,9 @@ struct SolveArgs {
     // the pass loop kept ~70 more VGPRs live in every solver kernel -- the
     // volcano kernel went from 158 to 227, i.e. from 3 to 2 waves per SIMD.)
     const int64_t* idx; const int32_t* nidx;
+    // 1: the degenerate-root retry above; 2: the screening pass's second
+    // launch (pck_solve_params.screen_rtol): the listed conditions solved
+    // exactly as a single pass would, nsteps adding the screening pass's
     int retry_pass;
     // cost-ordered dispatch (pck_solve_params.wave_order): block b of the lane
     // solver (one wavefront) solves the 64 conditions of wavefront worder[b]
@@ -1332,8 +1353,8 @@ __global__ void __launch_bounds__(PCK_SOLVE_BLOCK) __attribute__((amdgpu_waves_p
         if (!drc) {
             // retry pass: a completed transient is the degenerate root's answer;
             // a failed one keeps the first pass's outputs (PCK_ST_NEWTON_LOOSE)
-            const bool keep = a.retry_pass && st != PCK_ST_OK;
-            if (a.retry_pass) st = keep ? PCK_ST_NEWTON_LOOSE : PCK_ST_NEWTON;
+            const bool keep = a.retry_pass == 1 && st != PCK_ST_OK;
+            if (a.retry_pass == 1) st = keep ? PCK_ST_NEWTON_LOOSE : PCK_ST_NEWTON;
             if (a.y && !keep) {
 #pragma unroll
                 for (int i = 0; i < NS; ++i) a.y[i * a.ld_y + c] = y[i];

@@ -182,10 +182,12 @@ class DeviceNetwork:
 
     @staticmethod
     def params(t_end, t0=0.0, rtol=1e-8, atol=1e-10, max_steps=100000, newton=False, newton_iters=60,
-               activity=False, drc_eps=1e-3, retry=None, wave_order=0, root_dist=0.0):
+               activity=False, drc_eps=1e-3, retry=None, wave_order=0, root_dist=0.0, screen=None):
         """retry = (rtol, atol): with newton, the conditions whose polish meets a
         degenerate root (status 4) are integrated again at these tolerances
-        and report that transient end (pck_solve_params.retry_rtol)."""
+        and report that transient end (pck_solve_params.retry_rtol).
+        screen = (rtol, margin): the screening pass of steady solves
+        (pck_solve_params.screen_rtol / screen_margin)."""
         p = L.SolveParams()
         p.t0, p.t_end, p.rtol, p.atol = float(t0), float(t_end), float(rtol), float(atol)
         p.max_steps, p.newton, p.newton_iters = int(max_steps), int(bool(newton)), int(newton_iters)
@@ -194,6 +196,8 @@ class DeviceNetwork:
             p.retry_rtol, p.retry_atol = float(retry[0]), float(retry[1])
         p.wave_order = int(wave_order)     # 0 auto, 1 on, -1 off (pck_solve_params.wave_order)
         p.root_dist = float(root_dist)     # newton: the root only if the transient reached it
+        if screen is not None:
+            p.screen_rtol, p.screen_margin = float(screen[0]), float(screen[1])
         return p
 
     def solve(self, n, T, p, y0, desc=None, fixc=None, inflow=None, want_k=False, out=None, t_out=None, **kw):

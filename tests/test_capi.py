@@ -90,10 +90,19 @@ def _kernel_metadata(lib_path, tmp_path):
     cp = str(tmp_path / 'lib_copy.so')
     shutil.copyfile(lib_path, cp)
     subprocess.run(['objcopy', '--dump-section', '.hip_fatbin=' + fb, cp], check=True)
-    subprocess.run([LLVM + '/clang-offload-bundler', '--type=o', '--input=' + fb,
-                    '--targets=hipv4-amdgcn-amd-amdhsa--gfx950', '--output=' + elf, '--unbundle'], check=True)
-    notes = subprocess.run([LLVM + '/llvm-readelf', '--notes', elf], check=True, capture_output=True,
-                           text=True).stdout
+    # one offload bundle per translation unit of the split build (csrc/mk_inst.h)
+    blob = open(fb, 'rb').read()
+    magic = b'__CLANG_OFFLOAD_BUNDLE__'
+    starts = [m.start() for m in re.finditer(re.escape(magic), blob)]
+    assert starts, 'no offload bundle in the library'
+    notes = ''
+    for i, a in enumerate(starts):
+        part = str(tmp_path / ('fb%d.bin' % i))
+        open(part, 'wb').write(blob[a:starts[i + 1] if i + 1 < len(starts) else len(blob)])
+        subprocess.run([LLVM + '/clang-offload-bundler', '--type=o', '--input=' + part,
+                        '--targets=hipv4-amdgcn-amd-amdhsa--gfx950', '--output=' + elf, '--unbundle'], check=True)
+        notes += subprocess.run([LLVM + '/llvm-readelf', '--notes', elf], check=True, capture_output=True,
+                                text=True).stdout
     out = {}
     for b in notes.split('  - .agpr_count:')[1:]:
         g = lambda k: int(re.search(r'\.' + k + r':\s+(\d+)', b).group(1))
