@@ -47,7 +47,7 @@ DEGENERATE_RETRY = STEADY_TRANSIENT
 # STEADY_TRANSIENT exactly as without screening.  A transient that has settled
 # on its root ends on it at any tolerance, so the accepted conditions report
 # the same root.
-SCREEN_RTOL = 1.0e-3
+SCREEN_RTOL = 1.0e-2
 SCREEN_MARGIN = 0.1
 
 

@@ -201,8 +201,9 @@ __device__ __forceinline__ double rcp1(double x) {
 // the threshold-pivoting lu): the pivot reciprocals, 1/h and the projection
 // factor from rcp1; the threshold rule's pivot search only where some lane of
 // the wavefront needs it (one max per row and one compare per column on the
-// common path); the stage right-hand sides with the 1/h-scaled coefficients
-// computed once per step; the step-size factor from v_log_f32 / v_exp_f32.
+// common path); the step-size factor from v_log_f32 / v_exp_f32.  (The stage
+// right-hand sides with the 1/h-scaled coefficients computed once per step
+// saved 5 instructions and cost 8 VGPRs: not kept.)
 // 0 = the round-4 arithmetic (A/B).  Results move by rounding only.
 #ifndef PCK_LANE_FAST
 #define PCK_LANE_FAST 1

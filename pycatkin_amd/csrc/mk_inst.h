@@ -11,7 +11,9 @@
 
 // k_solve over the runtime plan of NS = 1..8 dynamic species, with the
 // evaluation kernels of the same NS
-#define PCK_INST_LANE_RT(X) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8)
+#define PCK_INST_LANE_RT_A(X) X(1) X(2) X(3) X(4)
+#define PCK_INST_LANE_RT_B(X) X(5) X(6) X(7) X(8)
+#define PCK_INST_LANE_RT(X) PCK_INST_LANE_RT_A(X) PCK_INST_LANE_RT_B(X)
 // lane-group kernels: (NSP, G, P) of PCK_GRP_SWITCH
 #define PCK_INST_GRP(X) X(16, 16, 1) X(32, 32, 1) X(64, 64, 1)
 

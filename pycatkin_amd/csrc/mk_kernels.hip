@@ -1065,6 +1065,16 @@ static int launch_solve(const pck_network* net, const pck_conditions* cond, cons
     }
     const bool grp = drc_groups || use_group(net, a.G);
     screen = screen && !grp;
+    // the screening pass inside the solve (the default: a lane that fails it
+    // solves again at once, so the slow second solves overlap the bulk of the
+    // first pass) or as two launches (PCK_SCREEN_INLINE=0, A/B)
+    const bool screen_inline = screen && !(getenv("PCK_SCREEN_INLINE") && getenv("PCK_SCREEN_INLINE")[0] == '0');
+    if (screen_inline) {
+        a.screen_rtol = prm->screen_rtol;
+        a.screen_atol = a.atol * (prm->screen_rtol / a.rtol);
+        a.screen_dist = a.root_dist * (prm->screen_margin > 0.0 ? prm->screen_margin : 0.1);
+        screen = false;
+    }
     if (grp && !net->grp_ok)
         return fail(PCK_E_SIZE, "lane-group solver: a reaction has more than 6 dynamic participants%s", "");
     GrpArgs ga;
@@ -1100,6 +1110,7 @@ static int launch_solve(const pck_network* net, const pck_conditions* cond, cons
                            n, W, list, cnt);
         HIPCHK(hipGetLastError());
         SolveArgs pv = a;
+        pv.screen_rtol = 0.0;
         // the preview's rtol floor: 1e-2 (the preview is latency-bound on its
         // slowest sample: ~80 steps there against ~120 at 1e-3; the volcano
         // step 5.71 -> 5.65 ms with the coarser order, profiles/r4/ab_preview_*);

@@ -572,44 +572,28 @@ __device__ PCK_LANE_INLINE int integrate(const P& p, const Lane<P::NS>& L, const
             continue;
         }
         double k1[NS], k2[NS], k3[NS], k4[NS], k5[NS], u[NS], fu[NS];
-        // the stage coefficients C_ij / h, once per step (PCK_LANE_FAST): every
-        // stage right-hand side is then a chain of FMAs on f(u_i)
-        const double h21 = PCK_LANE_FAST ? ih * C21 : 0.0, h31 = PCK_LANE_FAST ? ih * C31 : 0.0,
-                     h32 = PCK_LANE_FAST ? ih * C32 : 0.0, h41 = PCK_LANE_FAST ? ih * C41 : 0.0,
-                     h42 = PCK_LANE_FAST ? ih * C42 : 0.0, h43 = PCK_LANE_FAST ? ih * C43 : 0.0,
-                     h51 = PCK_LANE_FAST ? ih * C51 : 0.0, h52 = PCK_LANE_FAST ? ih * C52 : 0.0,
-                     h53 = PCK_LANE_FAST ? ih * C53 : 0.0, h54 = PCK_LANE_FAST ? ih * C54 : 0.0,
-                     h61 = PCK_LANE_FAST ? ih * C61 : 0.0, h62 = PCK_LANE_FAST ? ih * C62 : 0.0,
-                     h63 = PCK_LANE_FAST ? ih * C63 : 0.0, h64 = PCK_LANE_FAST ? ih * C64 : 0.0,
-                     h65 = PCK_LANE_FAST ? ih * C65 : 0.0;
 #pragma unroll
         for (int i = 0; i < NS; ++i) k1[i] = F0[i];
         if (PCK_CONS_ROWS && crows) cons_zero(p, k1);
         PCK_LPH(2, lu_solve<NS>(W, piv, sw, k1));
         PCK_LPH(4, for (int i = 0; i < NS; ++i) u[i] = y[i] + a21 * k1[i]);
         PCK_LPH(3, rhs(p, L, k, u, fu));
-        PCK_LPH(4, for (int i = 0; i < NS; ++i)
-                       k2[i] = PCK_LANE_FAST ? fu[i] + h21 * k1[i] : fu[i] + ih * (C21 * k1[i]));
+        PCK_LPH(4, for (int i = 0; i < NS; ++i) k2[i] = fu[i] + ih * (C21 * k1[i]));
         if (PCK_CONS_ROWS && crows) cons_zero(p, k2);
         PCK_LPH(2, lu_solve<NS>(W, piv, sw, k2));
         PCK_LPH(4, for (int i = 0; i < NS; ++i) u[i] = y[i] + a31 * k1[i] + a32 * k2[i]);
         PCK_LPH(3, rhs(p, L, k, u, fu));
-        PCK_LPH(4, for (int i = 0; i < NS; ++i)
-                       k3[i] = PCK_LANE_FAST ? fu[i] + h31 * k1[i] + h32 * k2[i] : fu[i] + ih * (C31 * k1[i] + C32 * k2[i]));
+        PCK_LPH(4, for (int i = 0; i < NS; ++i) k3[i] = fu[i] + ih * (C31 * k1[i] + C32 * k2[i]));
         if (PCK_CONS_ROWS && crows) cons_zero(p, k3);
         PCK_LPH(2, lu_solve<NS>(W, piv, sw, k3));
         PCK_LPH(4, for (int i = 0; i < NS; ++i) u[i] = y[i] + a41 * k1[i] + a42 * k2[i] + a43 * k3[i]);
         PCK_LPH(3, rhs(p, L, k, u, fu));
-        PCK_LPH(4, for (int i = 0; i < NS; ++i)
-                       k4[i] = PCK_LANE_FAST ? fu[i] + h41 * k1[i] + h42 * k2[i] + h43 * k3[i]
-                                             : fu[i] + ih * (C41 * k1[i] + C42 * k2[i] + C43 * k3[i]));
+        PCK_LPH(4, for (int i = 0; i < NS; ++i) k4[i] = fu[i] + ih * (C41 * k1[i] + C42 * k2[i] + C43 * k3[i]));
         if (PCK_CONS_ROWS && crows) cons_zero(p, k4);
         PCK_LPH(2, lu_solve<NS>(W, piv, sw, k4));
         PCK_LPH(4, for (int i = 0; i < NS; ++i) u[i] = y[i] + a51 * k1[i] + a52 * k2[i] + a53 * k3[i] + a54 * k4[i]);
         PCK_LPH(3, rhs(p, L, k, u, fu));
-        PCK_LPH(4, for (int i = 0; i < NS; ++i)
-                       k5[i] = PCK_LANE_FAST ? fu[i] + h51 * k1[i] + h52 * k2[i] + h53 * k3[i] + h54 * k4[i]
-                                             : fu[i] + ih * (C51 * k1[i] + C52 * k2[i] + C53 * k3[i] + C54 * k4[i]));
+        PCK_LPH(4, for (int i = 0; i < NS; ++i) k5[i] = fu[i] + ih * (C51 * k1[i] + C52 * k2[i] + C53 * k3[i] + C54 * k4[i]));
         if (PCK_CONS_ROWS && crows) cons_zero(p, k5);
         PCK_LPH(2, lu_solve<NS>(W, piv, sw, k5));
         double d2[TRAJ ? NS : 1], d3[TRAJ ? NS : 1];
@@ -625,9 +609,7 @@ __device__ PCK_LANE_INLINE int integrate(const P& p, const Lane<P::NS>& L, const
         PCK_LPH(3, rhs(p, L, k, u, fu));
         // k6 reuses k5's registers once k5 is folded into u
         PCK_LPH(4, for (int i = 0; i < NS; ++i)
-                       k5[i] = PCK_LANE_FAST
-                                   ? fu[i] + h61 * k1[i] + h62 * k2[i] + h63 * k3[i] + h64 * k4[i] + h65 * k5[i]
-                                   : fu[i] + ih * (C61 * k1[i] + C62 * k2[i] + C63 * k3[i] + C64 * k4[i] + C65 * k5[i]));
+                       k5[i] = fu[i] + ih * (C61 * k1[i] + C62 * k2[i] + C63 * k3[i] + C64 * k4[i] + C65 * k5[i]));
         if (PCK_CONS_ROWS && crows) cons_zero(p, k5);
         PCK_LPH(2, lu_solve<NS>(W, piv, sw, k5));
         PCK_LPH_MARK();
@@ -1249,6 +1231,12 @@ struct SolveArgs {
     // cost-ordered dispatch (pck_solve_params.wave_order): block b of the lane
     // solver (one wavefront) solves the 64 conditions of wavefront worder[b]
     const int32_t* worder;
+    // screening pass inside the solve (pck_solve_params.screen_rtol, one
+    // launch): every lane first runs the rule at screen_rtol / screen_atol
+    // with root distance screen_dist; a lane whose screening answer is not
+    // an accepted root solves again from y0 at rtol / atol / root_dist, in
+    // the same launch (screen_rtol 0: a single pass)
+    double screen_rtol, screen_atol, screen_dist;
 };
 
 // One condition's solve: transient from y0, then (with a.newton) the Newton
@@ -1258,10 +1246,28 @@ __device__ __forceinline__ int solve_lane(const P& p, const Lane<P::NS>& L, cons
                                           int64_t c, const SolveArgs& a, double (&y)[P::NS], int& ns,
                                           const TrajOut& to) {
     constexpr int NS = P::NS;
+    // the screening trip and the full solve are two inlined copies of the
+    // integrator (one copy in a two-trip loop kept the Newton polish's values
+    // live through the integrator: 223 VGPRs against 165)
+    int st, total = 0, nsp = 0;
+    if (!TRAJ && a.screen_rtol > 0.0) {
+#pragma unroll
+        for (int i = 0; i < NS; ++i) y[i] = cv.y0[i * cv.ld_y0 + c * cv.s_y0];
+        st = integrate<TRAJ>(p, L, k, y, a.t0, a.t_end, a.screen_rtol, a.screen_atol, a.max_steps, nsp,
+                             a.cons_rows != 0, to);
+        if (st == PCK_ST_OK && a.newton) st = newton(p, L, k, y, a.newton_iters, a.screen_dist, a.screen_atol);
+        total = nsp;
+        if (st == PCK_ST_OK) {
+            ns = total;
+            return st;
+        }
+    }
 #pragma unroll
     for (int i = 0; i < NS; ++i) y[i] = cv.y0[i * cv.ld_y0 + c * cv.s_y0];
-    int st = integrate<TRAJ>(p, L, k, y, a.t0, a.t_end, a.rtol, a.atol, a.max_steps, ns, a.cons_rows != 0, to);
+    st = integrate<TRAJ>(p, L, k, y, a.t0, a.t_end, a.rtol, a.atol, a.max_steps, nsp, a.cons_rows != 0, to);
     if (st == PCK_ST_OK && a.newton) st = newton(p, L, k, y, a.newton_iters, a.root_dist, a.atol);
+    total += nsp;
+    ns = total;
     return st;
 }
 

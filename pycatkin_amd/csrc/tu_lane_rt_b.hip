@@ -1,9 +1,9 @@
-// Translation unit of the runtime-plan lane kernels (csrc/mk_inst.h; the
+// Translation unit of the runtime-plan lane kernels of NS = 5..8 (csrc/mk_inst.h; the
 // parallel product build of __graft_entry__.build).
 #define PCK_KERNEL_TU 1
 #include "mk_inst.h"
 namespace pck {
 #define PCK_X(N) PCK_DO_LANE_RT(, N)
-PCK_INST_LANE_RT(PCK_X)
+PCK_INST_LANE_RT_B(PCK_X)
 #undef PCK_X
 }  // namespace pck

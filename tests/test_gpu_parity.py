@@ -674,3 +674,109 @@ def test_wave_order_ragged_and_tiny_batches(P, inputs, n):
     for k in ('y', 'tof', 'status', 'nsteps'):
         np.testing.assert_array_equal(res[1][k], res[-1][k])
     assert np.all((res[1]['status'] == 0) | (res[1]['status'] == 4))
+
+
+def _screen_solve(P, inputs, n, eco, eo, screen, retry=None):
+    """pck_solve of the volcano steady rule on the given points, with the
+    screening pass (screen = (rtol, margin)) or without (None)."""
+    import torch
+    import ctypes as C
+    from pycatkin_amd.functions.volcano import set_volcano_energies
+    from pycatkin_amd import _lib as L
+    from pycatkin_amd.engine import _ptr
+    from pycatkin_amd.classes.system import ROOT_DIST, STEADY_TRANSIENT
+    s = P.read_from_input_file(os.path.join(inputs, 'COOxVolcano', 'input.json'))
+    set_volcano_energies(s)
+    plan = s.plan(('CO_ox',))
+    net = s.device(('CO_ox',))
+    m = max(n, 1)
+    T, p, d, fx, y0, inflow = s._inputs(net, plan, m, np.full(m, 600.0), None, {'ECO': eco, 'EO': eo},
+                                        None, None, None)
+    cond, keep = net.conditions(m, T, p, d, fx, y0, inflow)
+    cond.n = n
+    out = dict(y=torch.full((net.NDYN, m), -7.0, dtype=torch.float64, device='cuda'),
+               tof=torch.full((m,), -7.0, dtype=torch.float64, device='cuda'),
+               status=torch.full((m,), -7, dtype=torch.int32, device='cuda'),
+               nsteps=torch.full((m,), -7, dtype=torch.int32, device='cuda'))
+    o = L.Outputs()
+    o.y, o.ld_y, o.tof, o.status, o.nsteps = _ptr(out['y']), m, _ptr(out['tof']), _ptr(out['status']), \
+        _ptr(out['nsteps'])
+    prm = net.params(t0=0.0, t_end=3600.0, rtol=STEADY_TRANSIENT[0], atol=STEADY_TRANSIENT[1], max_steps=200000,
+                     newton=True, root_dist=ROOT_DIST, screen=screen, retry=retry, activity=True)
+    rc = net.lib.pck_solve(net.h, C.byref(cond), C.byref(prm), C.byref(o),
+                           C.c_void_p(torch.cuda.current_stream().cuda_stream))
+    if rc:
+        return rc
+    torch.cuda.synchronize()
+    return {k: v.cpu().numpy() for k, v in out.items()}
+
+
+def _assert_screen_equivalent(a, b, label):
+    """The screening pass reports what the single pass reports: the same
+    status everywhere, the same root (to the Newton refinement's rounding) on
+    reached nodes, and bitwise the same transient end elsewhere (the second
+    launch runs the single pass's solve on those conditions)."""
+    pairs = {}
+    for x, y in zip(a['status'].tolist(), b['status'].tolist()):
+        pairs['%d->%d' % (x, y)] = pairs.get('%d->%d' % (x, y), 0) + 1
+    assert np.array_equal(a['status'], b['status']), (label, pairs)
+    ok = a['status'] == 0
+    rel = np.abs(b['tof'][ok] - a['tof'][ok]) / np.abs(a['tof'][ok])
+    assert rel.max(initial=0.0) <= 1e-10, (label, rel.max())
+    ry = np.abs(b['y'][:, ok] - a['y'][:, ok]) / np.maximum(np.abs(a['y'][:, ok]), 1e-300)
+    assert ry.max(initial=0.0) <= 1e-8, (label, ry.max())
+    rest = ~ok
+    np.testing.assert_array_equal(b['tof'][rest], a['tof'][rest])
+    np.testing.assert_array_equal(b['y'][:, rest], a['y'][:, rest])
+
+
+def test_screening_pass_matches_single_pass(P, inputs):
+    """pck_solve_params.screen_rtol (the default of System.solve_batch's
+    steady solves): the rule at rtol 1e-3, a root accepted only within 0.1 x
+    ROOT_DIST of that transient's end, then the single pass over the rest.
+    On a 512 x 512 volcano grid (patch order, cost-ordered dispatch, the
+    bistable poisoned corner included) it reports the single pass's answer at
+    every node (the full 1024 x 1024 grid: 0 of 1 048 576 statuses differ,
+    roots within 8.3e-14; tools/screen_check.py, profiles/r5/screen_check_*)."""
+    from pycatkin_amd.functions.volcano import tile_order
+    from pycatkin_amd.classes.system import SCREEN_MARGIN, SCREEN_RTOL
+    G = 512
+    be = np.linspace(-2.5, 0.5, G)
+    E1, E2 = np.meshgrid(be, be, indexing='ij')
+    perm = tile_order(E1.shape)
+    eco, eo = E1.ravel()[perm], E2.ravel()[perm]
+    a = _screen_solve(P, inputs, eco.size, eco, eo, None)
+    b = _screen_solve(P, inputs, eco.size, eco, eo, (SCREEN_RTOL, SCREEN_MARGIN))
+    _assert_screen_equivalent(a, b, 'grid 512')
+    assert np.mean(a['status'] == 0) > 0.8 and np.any(a['status'] == 4)
+    # both passes' steps are counted; the screened solve takes far fewer in all
+    assert b['nsteps'].astype(np.int64).sum() < 0.7 * a['nsteps'].astype(np.int64).sum()
+
+
+@pytest.mark.parametrize('n', [0, 1, 63, 2381])
+def test_screening_pass_ragged_and_tiny_batches(P, inputs, n):
+    """The screening pass on empty, single, short and ragged batches of random
+    volcano points: the single pass's answers, and n = 0 writes nothing."""
+    from pycatkin_amd.classes.system import SCREEN_MARGIN, SCREEN_RTOL
+    rng = np.random.default_rng(17)
+    m = max(n, 1)
+    eco, eo = rng.uniform(-2.5, 0.5, m), rng.uniform(-2.5, 0.5, m)
+    a = _screen_solve(P, inputs, n, eco, eo, None)
+    b = _screen_solve(P, inputs, n, eco, eo, (SCREEN_RTOL, SCREEN_MARGIN))
+    if n == 0:
+        assert np.all(b['status'] == -7) and np.all(b['tof'] == -7.0)
+        return
+    _assert_screen_equivalent(a, b, 'n=%d' % n)
+
+
+def test_screening_pass_argument_checks(P, inputs):
+    """screen_rtol with retry_rtol, a negative screen_rtol or a margin above 1
+    are PCK_E_ARG; a screen_rtol not above the transient rtol is a single pass."""
+    eco, eo = np.array([-1.0, -0.5]), np.array([-1.0, -1.5])
+    assert _screen_solve(P, inputs, 2, eco, eo, (1e-3, 0.1), retry=(1e-6, 1e-22)) == -1
+    assert _screen_solve(P, inputs, 2, eco, eo, (-1e-3, 0.1)) == -1
+    assert _screen_solve(P, inputs, 2, eco, eo, (1e-3, 1.5)) == -1
+    a = _screen_solve(P, inputs, 2, eco, eo, None)
+    b = _screen_solve(P, inputs, 2, eco, eo, (1e-7, 0.1))
+    for k in ('y', 'tof', 'status', 'nsteps'):
+        np.testing.assert_array_equal(a[k], b[k])

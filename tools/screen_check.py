@@ -2,7 +2,7 @@
 the single pass on the bench workload -- the 1024 x 1024 COOxVolcano grid
 (patch order, cost-ordered dispatch, steady rule) -- node by node.
 
-    python tools/screen_check.py [OUT.json] [--screen RTOL] [--margin M]
+    python tools/screen_check.py [OUT.json] [--screen RTOL] [--margin M] [--config volcano|cstr]
 
 Reports the status pairs (single, screened), the largest relative activity
 difference on nodes with equal status (roots: the same root to rounding;
@@ -23,6 +23,11 @@ sys.path.insert(0, ROOT)
 def main():
     args = sys.argv[1:]
     opt = {}
+    config = 'volcano'
+    if '--config' in args:
+        i = args.index('--config')
+        config = args[i + 1]
+        del args[i:i + 2]
     for k in ('--screen', '--margin', '--grid'):
         if k in args:
             i = args.index(k)
@@ -35,13 +40,21 @@ def main():
     if '--margin' in opt:
         S.SCREEN_MARGIN = opt['--margin']
     G = int(opt.get('--grid', 1024))
-    s = P.read_from_input_file(os.path.join(ROOT, 'tests', 'golden', 'inputs', 'COOxVolcano', 'input.json'))
-    set_volcano_energies(s)
-    be = np.linspace(-2.5, 0.5, G)
-    ECO, EO = np.meshgrid(be, be, indexing='ij')
-    order = tile_order((G, G))
-    kw = dict(T=np.full(order.size, 600.0), desc={'ECO': ECO.ravel()[order], 'EO': EO.ravel()[order]},
-              tof_terms=('CO_ox',), steady=True, activity=True)
+    if config == 'cstr':
+        # the bench's CSTR sweep (COOxReactor Pd111, 1e4 temperatures, steady rule)
+        s = P.read_from_input_file(os.path.join(ROOT, 'tests', 'golden', 'inputs', 'COOxReactor', 'input_Pd111.json'))
+        T = np.linspace(423.0, 623.0, 10000)
+        order = np.arange(T.size)
+        ECO = EO = np.full(T.size, np.nan)
+        kw = dict(T=T, tof_terms=('CO_ox',), steady=True, activity=False)
+    else:
+        s = P.read_from_input_file(os.path.join(ROOT, 'tests', 'golden', 'inputs', 'COOxVolcano', 'input.json'))
+        set_volcano_energies(s)
+        be = np.linspace(-2.5, 0.5, G)
+        ECO, EO = np.meshgrid(be, be, indexing='ij')
+        order = tile_order((G, G))
+        kw = dict(T=np.full(order.size, 600.0), desc={'ECO': ECO.ravel()[order], 'EO': EO.ravel()[order]},
+                  tof_terms=('CO_ox',), steady=True, activity=True)
     res = {}
     for name, scr in (('single', None), ('screened', opt.get('--screen', S.SCREEN_RTOL))):
         s.solve_batch(screen=scr, **kw)                       # warm (hipRTC, allocator)
@@ -58,7 +71,7 @@ def main():
     same = a['status'] == b['status']
     rel = np.abs(b['tof'] - a['tof']) / np.maximum(np.abs(a['tof']), 1e-300)
     diff = np.nonzero(~same)[0]
-    out = dict(grid=G, screen_rtol=opt.get('--screen', S.SCREEN_RTOL), margin=S.SCREEN_MARGIN,
+    out = dict(config=config, grid=G, screen_rtol=opt.get('--screen', S.SCREEN_RTOL), margin=S.SCREEN_MARGIN,
                wall_ms={k: v['wall_ms'] for k, v in res.items()},
                steps={k: int(v['nsteps'].astype(np.int64).sum()) for k, v in res.items()},
                status_pairs=pairs, n_status_differs=int(diff.size),
