@@ -336,7 +336,8 @@ def _solve_workload(wl, sim, net, plan, n, T, p, desc, tof_terms, steady, activi
     # solver launches per step: the first pass, the degenerate-root retry and,
     # on the lane solver with cost-ordered dispatch, its preview
     ordered = net.NDYN <= 8 and (wl.prm.wave_order == 1 or (wl.prm.wave_order == 0 and n >= 262144))
-    screened = net.NDYN <= 8 and wl.prm.screen_rtol > 0.0
+    # (the screening pass is a second launch only with PCK_SCREEN_INLINE=0)
+    screened = net.NDYN <= 8 and wl.prm.screen_rtol > 0.0 and os.environ.get('PCK_SCREEN_INLINE', '1') == '0'
     wl.solver_launches = 1 + int(bool(wl.prm.newton and wl.prm.retry_rtol > 0.0)) + int(ordered) + int(screened)
     wl.out, wl.o = _outputs(torch, net, n, L, _ptr)
     wl.kf = torch.empty((max(net.NRXN, 1), max(n, 1)), dtype=torch.float64, device='cuda')

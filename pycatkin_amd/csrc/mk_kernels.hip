@@ -206,6 +206,15 @@ extern "C" int pck_lphase_get(double* host8) {
     return PCK_OK;
 }
 #endif
+#if PCK_WAVE_TIMES
+// diagnostic builds only (-DPCK_WAVE_TIMES=1): the lane solver's wave
+// timeline (mk_solver.h), read by tools/wave_timeline.py
+extern "C" int pck_wtimes_get(long long* host, int n) {
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpyFromSymbol(host, HIP_SYMBOL(pck_wtimes), sizeof(long long) * 3 * (size_t)(n < PCK_WT_N ? n : PCK_WT_N)));
+    return PCK_OK;
+}
+#endif
 extern "C" const char* pck_last_error(void) { return g_err; }
 
 extern "C" int pck_network_create(const int32_t* ip, int64_t n_ip, const double* dp, int64_t n_dp,
@@ -792,19 +801,33 @@ __global__ void __launch_bounds__(256) k_select_status(int64_t n, const int32_t*
 // volcano patch) as a loose transient; max of their step counts is the
 // wavefront's key (tools/predictor_eval.py: 1.167x in the model against 1.170x
 // for the true costs).
-constexpr int PCK_PREVIEW_LANES = 4;
+// With the screening pass (round 5) a wavefront's cost is its screening
+// trips plus the full solves of the lanes the screening does not accept, so
+// the preview runs the screening trip itself (transient, Newton, the rule at
+// the screening distance) and a sample it does not accept adds
+// PCK_PREVIEW_REJECT (400) steps to the key.  With the transient-only
+// preview, wavefronts whose screening rejected lanes started mid-launch and
+// ended the launch 0.5 ms after the rest (tools/wave_timeline.py,
+// profiles/r5/wave_timeline_*): 2.71 -> 2.52 ms per 2^20 volcano step.
+// PCK_PREVIEW_LANES=8 samples rows 0, 5, 10, 15 x the patch's first and last
+// column instead of its 4 corners (A/B: 2.57 ms; the longer preview costs
+// more than the extra samples find).
+constexpr int PCK_PREVIEW_LANES_MAX = 8;
 // the preview lanes, the wavefront sort, k_select_ordered and k_solve's
 // worder mapping all take one block of the lane solver to be one wavefront
 static_assert(PCK_SOLVE_BLOCK == 64, "cost-ordered dispatch assumes one wavefront per lane-solver block");
-__device__ __forceinline__ int preview_lane(int k) { return (k < 2) ? 3 * k : 60 + 3 * (k - 2); }   // 0, 3, 60, 63
+__device__ __forceinline__ int preview_lane(int k, int np) {
+    if (np == 4) return (k < 2) ? 3 * k : 60 + 3 * (k - 2);      // 0, 3, 60, 63
+    return 20 * (k >> 1) + 3 * (k & 1);                            // 0, 3, 20, 23, 40, 43, 60, 63
+}
 
-__global__ void __launch_bounds__(256) k_preview_list(int64_t n, int64_t W, int64_t* list, int32_t* cnt) {
+__global__ void __launch_bounds__(256) k_preview_list(int64_t n, int64_t W, int np, int64_t* list, int32_t* cnt) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < W * PCK_PREVIEW_LANES) {
-        const int64_t c = (i / PCK_PREVIEW_LANES) * PCK_SOLVE_BLOCK + preview_lane((int)(i % PCK_PREVIEW_LANES));
+    if (i < W * np) {
+        const int64_t c = (i / np) * PCK_SOLVE_BLOCK + preview_lane((int)(i % np), np);
         list[i] = (c < n) ? c : n - 1;      // a short last wavefront samples its last condition
     }
-    if (i == 0) *cnt = (int32_t)(W * PCK_PREVIEW_LANES);
+    if (i == 0) *cnt = (int32_t)(W * np);
 }
 
 // (A grid-wide histogram / scan / scatter sort took 0.17 ms against the one-
@@ -815,15 +838,17 @@ __global__ void __launch_bounds__(256) k_preview_list(int64_t n, int64_t W, int6
 // gathered from the scattered preview outputs by the whole grid, so that the
 // one-block sort below reads W contiguous keys (it read 4 W scattered lines
 // itself: ~28 of its 70 us)
-__global__ void __launch_bounds__(256) k_wave_keys(int64_t n, int64_t W, const int32_t* ns, int32_t* wkey) {
+// st (screening previews): a sample whose screening trip is not accepted
+// counts `reject` more steps
+__global__ void __launch_bounds__(256) k_wave_keys(int64_t n, int64_t W, int np, const int32_t* ns,
+                                                   const int32_t* st, int reject, int32_t* wkey) {
     const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (w >= W) return;
     int k = 0;
-#pragma unroll
-    for (int l = 0; l < PCK_PREVIEW_LANES; ++l) {
-        int64_t c = w * PCK_SOLVE_BLOCK + preview_lane(l);
+    for (int l = 0; l < np; ++l) {
+        int64_t c = w * PCK_SOLVE_BLOCK + preview_lane(l, np);
         c = (c < n) ? c : n - 1;
-        k = max(k, ns[c]);
+        k = max(k, ns[c] + ((st && st[c] != PCK_ST_OK) ? reject : 0));
     }
     wkey[w] = min(max(k, 0), 1023);
 }
@@ -1098,16 +1123,24 @@ static int launch_solve(const pck_network* net, const pck_conditions* cond, cons
                        (prm->wave_order > 0 || (prm->wave_order == 0 && n >= 262144));
     if (order) {
         const int64_t W = (n + PCK_SOLVE_BLOCK - 1) / PCK_SOLVE_BLOCK;
-        const size_t b_list = sizeof(int64_t) * (size_t)W * PCK_PREVIEW_LANES, b_ns = sizeof(int32_t) * (size_t)n;
-        rc = salloc(oscr, b_list + 64 + b_ns + 2 * sizeof(int32_t) * (size_t)W, s);
+        int np = 4;
+        {
+            const char* e = getenv("PCK_PREVIEW_LANES");
+            if (e && atoi(e) == PCK_PREVIEW_LANES_MAX) np = PCK_PREVIEW_LANES_MAX;
+        }
+        // the preview runs the screening trip where the solve screens
+        const bool pscreen = a.screen_rtol > 0.0 && !(getenv("PCK_PREVIEW_RULE") && getenv("PCK_PREVIEW_RULE")[0] == '0');
+        const size_t b_list = sizeof(int64_t) * (size_t)W * np, b_ns = sizeof(int32_t) * (size_t)n;
+        rc = salloc(oscr, b_list + 64 + 2 * b_ns + 2 * sizeof(int32_t) * (size_t)W, s);
         if (rc) return rc;
         int64_t* list = oscr.as<int64_t>();
         int32_t* cnt = (int32_t*)((char*)list + b_list);
         int32_t* pns = (int32_t*)((char*)list + b_list + 64);
-        int32_t* wo = pns + n;
+        int32_t* pst = pns + n;                     // screening previews: the samples' statuses
+        int32_t* wo = pst + n;
         int32_t* wkey = wo + W;                     // per-wavefront sort key, compact
-        hipLaunchKernelGGL(k_preview_list, dim3((unsigned)((W * PCK_PREVIEW_LANES + 255) / 256)), dim3(256), 0, s,
-                           n, W, list, cnt);
+        hipLaunchKernelGGL(k_preview_list, dim3((unsigned)((W * np + 255) / 256)), dim3(256), 0, s,
+                           n, W, np, list, cnt);
         HIPCHK(hipGetLastError());
         SolveArgs pv = a;
         pv.screen_rtol = 0.0;
@@ -1127,16 +1160,33 @@ static int launch_solve(const pck_network* net, const pck_conditions* cond, cons
             if (e) pv.atol = fmax(pv.atol, atof(e) * pv.rtol);
         }
         pv.newton = 0;
+        if (pscreen) {                               // the screening trip, as the solve runs it
+            pv.rtol = a.screen_rtol;
+            pv.atol = a.screen_atol;
+            pv.newton = a.newton;
+            pv.root_dist = a.screen_dist;
+        }
         pv.max_steps = a.max_steps < 1000 ? a.max_steps : 1000;
-        pv.y = nullptr; pv.tof = nullptr; pv.status = nullptr; pv.nsteps = pns;
+        pv.y = nullptr; pv.tof = nullptr; pv.status = pscreen ? pst : nullptr; pv.nsteps = pns;
         pv.idx = list; pv.nidx = cnt; pv.retry_pass = 0; pv.worder = nullptr;
-        rc = run_solver(net, cond, pv, grp, ga, traj, kf, kr, s, W * PCK_PREVIEW_LANES);
+        rc = run_solver(net, cond, pv, grp, ga, traj, kf, kr, s, W * np);
         if (rc) return rc;
-        hipLaunchKernelGGL(k_wave_keys, dim3((unsigned)((W + 255) / 256)), dim3(256), 0, s, n, W, pns, wkey);
+        int reject = 400;
+        {
+            const char* e = getenv("PCK_PREVIEW_REJECT");
+            if (e) reject = atoi(e);
+        }
+        hipLaunchKernelGGL(k_wave_keys, dim3((unsigned)((W + 255) / 256)), dim3(256), 0, s, n, W, np, pns,
+                           pscreen ? pst : nullptr, reject, wkey);
         HIPCHK(hipGetLastError());
         hipLaunchKernelGGL(k_wave_order, dim3(1), dim3(1024), 0, s, W, wkey, wo);
         HIPCHK(hipGetLastError());
         a.worder = wo;
+        // issue priority for the costliest wavefronts (PCK_PRIO_WAVES: a
+        // count, or a fraction of the launch's wavefronts below 1)
+        const char* e = getenv("PCK_PRIO_WAVES");
+        const double pw = e ? atof(e) : 0.0;
+        a.prio_waves = (int)(pw < 1.0 ? pw * (double)W : pw);
     }
     StreamScratch rscr;
     if (retry || screen) {

@@ -88,6 +88,18 @@ __device__ double pck_lphase[8];
 #define PCK_LPH_UNTIL(i) do {} while (0)
 #define PCK_LPH_FLUSH() do {} while (0)
 #endif
+// Wave timeline (diagnostic builds, -DPCK_WAVE_TIMES=1; tools/wave_timeline.py):
+// every block of a lane-solver launch over the whole batch (no index list)
+// records [start, end] on the constant-rate real-time clock and its hardware
+// slot (HW_ID), for the first PCK_WT_N blocks of the last such launch
+#ifndef PCK_WAVE_TIMES
+#define PCK_WAVE_TIMES 0
+#endif
+#if PCK_WAVE_TIMES
+#define PCK_WT_N 65536
+__device__ long long pck_wtimes[3 * PCK_WT_N];
+#endif
+
 #define PCK_LRET(st)       \
     do {                   \
         PCK_LPH_FLUSH();   \
@@ -1237,6 +1249,9 @@ struct SolveArgs {
     // an accepted root solves again from y0 at rtol / atol / root_dist, in
     // the same launch (screen_rtol 0: a single pass)
     double screen_rtol, screen_atol, screen_dist;
+    // cost-ordered dispatch: the first prio_waves blocks of the order (the
+    // costliest wavefronts) raise their issue priority on the SIMD
+    int prio_waves;
 };
 
 // One condition's solve: transient from y0, then (with a.newton) the Newton
@@ -1319,6 +1334,13 @@ __global__ void __launch_bounds__(PCK_SOLVE_BLOCK) __attribute__((amdgpu_waves_p
         for (int i = threadIdx.x; i < nd; i += blockDim.x) lds[i] = __builtin_nan("");
         __syncthreads();
     }
+#endif
+    // the costliest wavefronts of a cost-ordered launch take issue priority
+    // over the rest of the SIMD's waves, so that they progress at near their
+    // own latency while the cheap waves fill the issue slots they leave
+    if (a.worder && (int)blockIdx.x < a.prio_waves) __builtin_amdgcn_s_setprio(2);
+#if PCK_WAVE_TIMES
+    const long long wt0 = __builtin_amdgcn_s_memrealtime();
 #endif
     const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int G = a.G;
@@ -1403,6 +1425,20 @@ __global__ void __launch_bounds__(PCK_SOLVE_BLOCK) __attribute__((amdgpu_waves_p
             if (a.nsteps) a.nsteps[c] = gns;
         }
     }
+#if PCK_WAVE_TIMES
+    {
+        int wmax = active ? ns : 0;                  // the wave's largest step count
+        for (int m = 1; m < 64; m <<= 1) wmax = max(wmax, __shfl_xor(wmax, m, 64));
+        if (!a.idx && (threadIdx.x & 63) == 0 && blockIdx.x < PCK_WT_N) {
+            const long long wt1 = __builtin_amdgcn_s_memrealtime();
+            pck_wtimes[3 * blockIdx.x] = wt0;
+            pck_wtimes[3 * blockIdx.x + 1] = wt1;
+            // HW_ID (high word) and the step count
+            pck_wtimes[3 * blockIdx.x + 2] =
+                ((long long)(unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4) << 32) | (unsigned)wmax;
+        }
+    }
+#endif
 }
 
 }  // namespace pck
