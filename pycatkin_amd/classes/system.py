@@ -49,6 +49,11 @@ DEGENERATE_RETRY = STEADY_TRANSIENT
 # the same root.
 SCREEN_RTOL = 1.0e-2
 SCREEN_MARGIN = 0.1
+# 'auto' screens the one-lane networks (<= 8 dynamic species: the volcano and
+# CSTR configs); the lane-group kernels screen too when asked (screen=rtol),
+# but a network that rarely reaches its root by t_end (the synthetic one
+# never does) would then solve most conditions twice
+SCREEN_MAX_LANE_SPECIES = 8
 
 
 def _retry_tolerances(retry):
@@ -472,7 +477,8 @@ class System:
         ('auto': SCREEN_RTOL for steady solves with root_dist > 0, no retry
         and no t_out; None: off; a number: the screening rtol) runs the rule
         at that loose tolerance first and solves only the conditions it does
-        not accept at the transient tolerances (one-lane networks)."""
+        not accept at the transient tolerances ('auto' on one-lane networks
+        only; a number screens lane-group networks too)."""
         plan = self.plan(tuple(tof_terms), None)
         net = self.device(tuple(tof_terms), None)
         sizes = [T, p] + (list(desc.values()) if desc else [])
@@ -493,7 +499,8 @@ class System:
         if isinstance(screen, str):
             if screen != 'auto':
                 raise ValueError("screen must be 'auto', None or an rtol")
-            screen = SCREEN_RTOL if (steady and root_dist > 0.0 and retry is None and t_out is None) else None
+            screen = SCREEN_RTOL if (steady and root_dist > 0.0 and retry is None and t_out is None
+                                     and net.NDYN <= SCREEN_MAX_LANE_SPECIES) else None
         out = net.solve(n, T, p, y0, d, fx, inflow, t0=t0, t_end=t_end,
                         rtol=self.params['rtol'] if rtol is None else rtol,
                         atol=self.params['atol'] if atol is None else atol,
@@ -506,12 +513,13 @@ class System:
         return out
 
     def drc_batch(self, tof_terms, T=None, p=None, desc=None, eps=1.0e-3, steady=False, t_end=None, rtol=None,
-                  atol=None, max_steps=200000, y0=None, fix=None, inflow=None):
+                  atol=None, max_steps=200000, y0=None, fix=None, inflow=None, screen='auto'):
         """Degree of rate control of every reaction (old_system.py:490-515) for a batch.
         steady=True: each of the 2R+1 solves is a steady-state solve with
         solve_batch's rule (STEADY_TRANSIENT unless rtol / atol are given;
         the root where the transient has reached it to ROOT_DIST, else the
-        transient end: the condition's status is then 4).
+        transient end: the condition's status is then 4).  `screen`: as in
+        solve_batch (each of the 2R+1 solves screened on its own).
 
         Returns {reaction name: xi [n]} (ghost reactions: 0) plus 'tof0' and 'status'."""
         plan = self.plan(tuple(tof_terms), None)
@@ -525,10 +533,15 @@ class System:
         if steady:
             rtol = STEADY_TRANSIENT[0] if rtol is None else rtol
             atol = STEADY_TRANSIENT[1] if atol is None else atol
+        if isinstance(screen, str):
+            if screen != 'auto':
+                raise ValueError("screen must be 'auto', None or an rtol")
+            screen = SCREEN_RTOL if (steady and net.NDYN <= SCREEN_MAX_LANE_SPECIES) else None
         r = net.drc(n, T, p, y0, d, fx, inflow, t0=times[0], t_end=times[-1] if t_end is None else t_end,
                     rtol=self.params['rtol'] if rtol is None else rtol,
                     atol=self.params['atol'] if atol is None else atol, max_steps=max_steps, newton=steady,
-                    drc_eps=eps, root_dist=ROOT_DIST if steady else 0.0)
+                    drc_eps=eps, root_dist=ROOT_DIST if steady else 0.0,
+                    screen=(float(screen), SCREEN_MARGIN) if (steady and screen) else None)
         xi = r['xi'].cpu().numpy()
         out = {name: (xi[plan.reactions.index(name)] if name in plan.reactions else np.zeros(n))
                for name in plan.all_reactions}

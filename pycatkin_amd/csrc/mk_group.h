@@ -1689,12 +1689,29 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 64
     TrajOut to{a.t_out, a.n_out, a.traj, a.ld_traj, c};
     LU<NSP> F;                  // one factorisation storage for the transient and the Newton polish
     // transient and polish (a degenerate root's retry transient is a second
-    // launch over the compacted list, mk_solver.h: SolveArgs::idx)
-    y = x.row ? cv.y0[x.gl * cv.ld_y0 + c * cv.s_y0] : 0.0;
-    int st = grp_integrate<NSP, G, P, TRAJ, Net>(nv, gl, x, y, a.t0, a.t_end, a.rtol, a.atol, a.max_steps, ns,
+    // launch over the compacted list, mk_solver.h: SolveArgs::idx); with the
+    // screening pass (SolveArgs::screen_rtol, mk_solver.h: solve_lane) first
+    // the rule at the screening tolerance, and the full solve only where it
+    // is not accepted (the decision is group-uniform)
+    int st = PCK_ST_NEWTON;
+    bool done = false;
+    if (!TRAJ && a.screen_rtol > 0.0) {
+        y = x.row ? cv.y0[x.gl * cv.ld_y0 + c * cv.s_y0] : 0.0;
+        st = grp_integrate<NSP, G, P, TRAJ, Net>(nv, gl, x, y, a.t0, a.t_end, a.screen_rtol, a.screen_atol,
+                                                 a.max_steps, ns, a.cons_rows != 0, to, F);
+        if (st == PCK_ST_OK && a.newton)
+            st = grp_newton<NSP, G, P, Net>(nv, gl, x, y, a.newton_iters, F, a.screen_dist, a.screen_atol);
+        done = (st == PCK_ST_OK);
+    }
+    if (!done) {
+        int nsp = 0;
+        y = x.row ? cv.y0[x.gl * cv.ld_y0 + c * cv.s_y0] : 0.0;
+        st = grp_integrate<NSP, G, P, TRAJ, Net>(nv, gl, x, y, a.t0, a.t_end, a.rtol, a.atol, a.max_steps, nsp,
                                                  a.cons_rows != 0, to, F);
-    if (st == PCK_ST_OK && a.newton)
-        st = grp_newton<NSP, G, P, Net>(nv, gl, x, y, a.newton_iters, F, a.root_dist, a.atol);
+        if (st == PCK_ST_OK && a.newton)
+            st = grp_newton<NSP, G, P, Net>(nv, gl, x, y, a.newton_iters, F, a.root_dist, a.atol);
+        ns += nsp;
+    }
     const double tof = grp_tof<NSP, G>(nv, gl, x, y);
     const bool fin = gmin<G>((!x.row || isfinite(y)) ? 1.0 : 0.0) > 0.0 && isfinite(tof);
     if (!fin && st == PCK_ST_OK) st = PCK_ST_NONFINITE;

@@ -1072,7 +1072,7 @@ static int launch_solve(const pck_network* net, const pck_conditions* cond, cons
     // loose tolerance with a tighter acceptance, then the single pass at the
     // caller's tolerances over the rest (one-lane path, pck_solve only)
     bool screen = prm->newton && prm->root_dist > 0.0 && prm->screen_rtol > 0.0 && prm->screen_rtol > prm->rtol &&
-                  !drc_groups && a.G == 1 && !traj;
+                  !traj;
     if (traj) {
         if (!prm->t_out) return fail(PCK_E_ARG, "n_out > 0 without t_out%s", "");
         if (drc_groups || a.G != 1) return fail(PCK_E_ARG, "trajectory output is for pck_solve only%s", "");
@@ -1089,11 +1089,12 @@ static int launch_solve(const pck_network* net, const pck_conditions* cond, cons
         a.cons_rows = (e && e[0] == '1');
     }
     const bool grp = drc_groups || use_group(net, a.G);
-    screen = screen && !grp;
-    // the screening pass inside the solve (the default: a lane that fails it
-    // solves again at once, so the slow second solves overlap the bulk of the
-    // first pass) or as two launches (PCK_SCREEN_INLINE=0, A/B)
-    const bool screen_inline = screen && !(getenv("PCK_SCREEN_INLINE") && getenv("PCK_SCREEN_INLINE")[0] == '0');
+    // the screening pass inside the solve (the default: a lane or group that
+    // fails it solves again at once, so the slow second solves overlap the
+    // bulk of the first pass) or, for pck_solve on the one-lane path, as two
+    // launches (PCK_SCREEN_INLINE=0, A/B)
+    const bool screen_inline =
+        screen && (grp || drc_groups || a.G != 1 || !(getenv("PCK_SCREEN_INLINE") && getenv("PCK_SCREEN_INLINE")[0] == '0'));
     if (screen_inline) {
         a.screen_rtol = prm->screen_rtol;
         a.screen_atol = a.atol * (prm->screen_rtol / a.rtol);
@@ -1182,6 +1183,12 @@ static int launch_solve(const pck_network* net, const pck_conditions* cond, cons
         hipLaunchKernelGGL(k_wave_order, dim3(1), dim3(1024), 0, s, W, wkey, wo);
         HIPCHK(hipGetLastError());
         a.worder = wo;
+        // A/B (PCK_SCREEN_SKIP=1): wavefronts with a rejected preview sample
+        // skip the screening trip
+        if (pscreen && getenv("PCK_SCREEN_SKIP") && getenv("PCK_SCREEN_SKIP")[0] == '1') {
+            a.wkey = wkey;
+            a.skip_key = reject;
+        }
         // issue priority for the costliest wavefronts (PCK_PRIO_WAVES: a
         // count, or a fraction of the launch's wavefronts below 1)
         const char* e = getenv("PCK_PRIO_WAVES");

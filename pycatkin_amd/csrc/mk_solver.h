@@ -1252,6 +1252,12 @@ struct SolveArgs {
     // cost-ordered dispatch: the first prio_waves blocks of the order (the
     // costliest wavefronts) raise their issue priority on the SIMD
     int prio_waves;
+    // screening with a screening-rule preview: a wavefront whose key is at
+    // least skip_key (some preview sample was not accepted) runs the single
+    // pass directly (its screening trip would lengthen the wave's critical
+    // path for nothing); wkey == nullptr: never
+    const int32_t* wkey;
+    int skip_key;
 };
 
 // One condition's solve: transient from y0, then (with a.newton) the Newton
@@ -1259,13 +1265,13 @@ struct SolveArgs {
 template <bool TRAJ, class P, class K>
 __device__ __forceinline__ int solve_lane(const P& p, const Lane<P::NS>& L, const K& k, const CondView& cv,
                                           int64_t c, const SolveArgs& a, double (&y)[P::NS], int& ns,
-                                          const TrajOut& to) {
+                                          const TrajOut& to, bool screen_on = true) {
     constexpr int NS = P::NS;
     // the screening trip and the full solve are two inlined copies of the
     // integrator (one copy in a two-trip loop kept the Newton polish's values
     // live through the integrator: 223 VGPRs against 165)
     int st, total = 0, nsp = 0;
-    if (!TRAJ && a.screen_rtol > 0.0) {
+    if (!TRAJ && a.screen_rtol > 0.0 && screen_on) {
 #pragma unroll
         for (int i = 0; i < NS; ++i) y[i] = cv.y0[i * cv.ld_y0 + c * cv.s_y0];
         st = integrate<TRAJ>(p, L, k, y, a.t0, a.t_end, a.screen_rtol, a.screen_atol, a.max_steps, nsp,
@@ -1372,7 +1378,8 @@ __global__ void __launch_bounds__(PCK_SOLVE_BLOCK) __attribute__((amdgpu_waves_p
         load_keff(p, nv, cv, c, kf, kr, ld_k, k, pj, pfac);
         double y[NS];
         TrajOut to{a.t_out, a.n_out, a.traj, a.ld_traj, c};
-        st = solve_lane<TRAJ>(p, L, k, cv, c, a, y, ns, to);
+        const bool screen_on = !(a.wkey && a.worder && a.wkey[a.worder[blockIdx.x]] >= a.skip_key);
+        st = solve_lane<TRAJ>(p, L, k, cv, c, a, y, ns, to, screen_on);
         tof = lane_tof(p, nv, k, y);
         bool fin = isfinite(tof);
 #pragma unroll

@@ -364,3 +364,21 @@ def test_trajectory_untouched_by_a_retry_pass(P, inputs):
     assert a['status'][0] == 4 and b['status'][0] in (4, 5)
     np.testing.assert_array_equal(a['traj'], b['traj'])
     assert not np.array_equal(a['y'], b['y'])       # the retry did re-integrate the end state
+
+
+def test_drc_screening_pass_matches_single_pass(P, inputs):
+    """drc_batch(steady=True) screens each of the 2R+1 lane solves on its own
+    ('auto' on the one-lane volcano network): statuses equal and the degrees
+    of rate control within 1e-8 of the single pass on a reached node, the
+    not-reached fixture node and a few grid points."""
+    s, eco, eo = _not_reached_node(P, inputs)
+    E1 = np.array([eco, -1.0, -1.5, -0.5, -2.0])
+    E2 = np.array([eo, -1.0, -0.5, -1.5, -0.25])
+    kw = dict(T=np.full(5, 600.0), desc={'ECO': E1, 'EO': E2}, eps=1e-3, steady=True)
+    a = s.drc_batch(('CO_ox',), screen=None, **kw)
+    b = s.drc_batch(('CO_ox',), **kw)
+    np.testing.assert_array_equal(a['status'], b['status'])
+    assert np.any(a['status'] == 0)
+    for name in s.reactions:
+        np.testing.assert_allclose(b[name], a[name], rtol=1e-8, atol=1e-10)
+    np.testing.assert_allclose(b['tof0'], a['tof0'], rtol=1e-10)

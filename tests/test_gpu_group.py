@@ -713,3 +713,26 @@ def test_balanced_walk_matches_row_loops(P, inputs, synthetic, monkeypatch):
     monkeypatch.delenv('PCK_GRP_BALANCE')
     assert np.all(a['status'] == 0) and np.all(b['status'] == 0)
     assert close(a['y'], b['y'], rtol=1e-7, floor=1e-13), np.abs(a['y'] - b['y']).max()
+
+
+def test_group_screening_pass_matches_single_pass(P, inputs):
+    """The screening pass on the lane-group kernel (System.solve_batch with
+    screen=rtol; 'auto' screens one-lane networks only): DMTM steady states
+    over a T x p grid -- the rule at rtol 1e-2 first, the full solve where it
+    is not accepted (group-uniform) -- report what the single pass reports:
+    the same statuses, the same roots to the refinement's rounding, the same
+    transient ends bitwise (mk_group.h: k_solve_grp)."""
+    from pycatkin_amd.classes.system import SCREEN_RTOL
+    s = _dmtm(P, inputs)
+    TT, pp = np.meshgrid(np.linspace(450.0, 750.0, 8), np.logspace(4.0, 6.0, 8), indexing='ij')
+    kw = dict(T=TT.ravel(), p=pp.ravel(), steady=True)
+    a = s.solve_batch(screen=None, **kw)
+    b = s.solve_batch(screen=SCREEN_RTOL, **kw)
+    assert np.array_equal(a['status'], b['status']), (a['status'], b['status'])
+    ok = a['status'] == 0
+    assert ok.mean() > 0.5
+    ry = np.abs(b['y'][:, ok] - a['y'][:, ok]) / np.maximum(np.abs(a['y'][:, ok]), 1e-300)
+    assert ry.max(initial=0.0) <= 1e-8, ry.max()
+    np.testing.assert_array_equal(b['y'][:, ~ok], a['y'][:, ~ok])
+    # the screened solve took fewer integrator steps (both trips counted)
+    assert b['nsteps'].astype(np.int64).sum() < a['nsteps'].astype(np.int64).sum()
