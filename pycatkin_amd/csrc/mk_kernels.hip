@@ -1164,6 +1164,14 @@ static int launch_solve(const pck_network* net, const pck_conditions* cond, cons
         if (pscreen) {                               // the screening trip, as the solve runs it
             pv.rtol = a.screen_rtol;
             pv.atol = a.screen_atol;
+            {
+                // A/B: PCK_PREVIEW_SCREEN_RTOL, a coarser preview of the trip
+                const char* e = getenv("PCK_PREVIEW_SCREEN_RTOL");
+                if (e && atof(e) > a.screen_rtol) {
+                    pv.atol = a.screen_atol * (atof(e) / a.screen_rtol);
+                    pv.rtol = atof(e);
+                }
+            }
             pv.newton = a.newton;
             pv.root_dist = a.screen_dist;
         }

@@ -29,6 +29,11 @@ def main():
         i = args.index('--lib')
         os.environ['PCK_LIB'] = os.path.abspath(args[i + 1])
         del args[i:i + 2]
+    screen = 'auto'
+    if '--screen' in args:                     # --screen 0: the single pass
+        i = args.index('--screen')
+        screen = float(args[i + 1]) or None
+        del args[i:i + 2]
     import torch
     import pycatkin_amd as P
     from pycatkin_amd import _lib as L
@@ -41,7 +46,7 @@ def main():
     ECO, EO = np.meshgrid(be, be, indexing='ij')
     order = tile_order((1024, 1024))
     kw = dict(T=np.full(order.size, 600.0), desc={'ECO': ECO.ravel()[order], 'EO': EO.ravel()[order]},
-              tof_terms=('CO_ox',), steady=True, activity=True, to_numpy=False)
+              tof_terms=('CO_ox',), steady=True, activity=True, to_numpy=False, screen=screen)
     s.solve_batch(**kw)                        # warm
     torch.cuda.synchronize()
     L.check(lib.pck_lphase_reset())
@@ -53,7 +58,7 @@ def main():
     L.check(lib.pck_lphase_get(ph.ctypes.data_as(C.c_void_p)))
     steps, waves = max(ph[6], 1.0), ph[7]
     tot = ph[:6].sum()
-    out = dict(workload='volcano 1024x1024 patch order, steady', wall_ms=1e3 * wall, sampled_waves=int(waves),
+    out = dict(workload='volcano 1024x1024 patch order, steady, screen %s' % screen, wall_ms=1e3 * wall, sampled_waves=int(waves),
                steps_per_wave=steps / max(waves, 1.0),
                cycles_per_step={n: ph[k] / steps for k, n in enumerate(NAMES)},
                share={n: ph[k] / tot for k, n in enumerate(NAMES)},
