@@ -44,6 +44,7 @@ struct pck_network {
     mutable std::atomic<bool> jit_on{false};      // the last lane solve ran the hipRTC-compiled plan
     mutable std::atomic<bool> grp_jit_on{false};  // the last lane-group solve ran the exact-size hipRTC kernel
     mutable std::atomic<bool> grp_ct_on{false};   // ... with the network compiled in (mk_group.h: ct_rhs)
+    mutable std::atomic<bool> grp_quad_on{false}; // ... the quad-group kernel (mk_quad.h)
 };
 
 // FNV-1a 64 over the solver-side structure (network.py: structural_digest)
@@ -491,7 +492,9 @@ extern "C" int pck_network_dims(const pck_network* net, int32_t* dims) {
     dims[0] = v.D; dims[1] = v.NTH; dims[2] = v.NREG; dims[3] = v.NRXN; dims[4] = v.NDYN;
     dims[5] = v.NFIX; dims[6] = v.NCONS; dims[7] = v.NTOF; dims[8] = v.nfeat;
     dims[9] = net->spec ? net->spec : net->jit_on.load(std::memory_order_relaxed) ? PCK_SPEC_JIT : 0;
-    dims[10] = net->grp_ct_on.load(std::memory_order_relaxed) ? 2 : net->grp_jit_on.load(std::memory_order_relaxed) ? 1 : 0;
+    dims[10] = net->grp_quad_on.load(std::memory_order_relaxed) ? 3
+               : net->grp_ct_on.load(std::memory_order_relaxed) ? 2
+               : net->grp_jit_on.load(std::memory_order_relaxed) ? 1 : 0;
     return PCK_OK;
 }
 
@@ -944,6 +947,32 @@ static int run_solver(const pck_network* net, const pck_conditions* cond, const 
         const int G = grp_g(NS);
         const int per = 64 / G;
         const int64_t groups = n * ga.M;
+        // transient solves of networks of at most 16 species: the quad-group
+        // kernel (mk_quad.h), four lanes per condition
+        if (NS <= 16 && !traj && !a.newton && !a.cons_rows && net->plan_mode != PCK_PLAN_RUNTIME && jit_enabled() &&
+            grp_quad_enabled(NS, net->nv.NRXN) && grp_ct_enabled(G, net->nv.NRXN) && !net->jit_grp_src.empty()) {
+            hipFunction_t fq = jit_group_quad_kernel(net->digest, net->jit_grp_src, net->grp_npmax, net->grp_emax);
+            if (fq) {
+                const int R1 = net->nv.NRXN > 0 ? net->nv.NRXN : 1;
+                const size_t shm = sizeof(double) * 16 * 2 * (size_t)R1;
+                if (shm > 64 * 1024)
+                    return fail(PCK_E_SIZE, "quad-group solver: %s%lld bytes of LDS per block", "", (long long)shm);
+                NetView nv = net->nv;
+                CondView cv = cview(cond);
+                const double* kfp = kf;
+                const double* krp = kr;
+                int64_t ldk = n;
+                void* args[] = {&nv, &cv, &kfp, &krp, &ldk, &a, &ga};
+                const unsigned nb = (unsigned)((groups + 15) / 16);
+                HIPCHK(hipModuleLaunchKernel(fq, nb, 1, 1, 64, 1, 1, (unsigned)shm, s, args, nullptr));
+                net->grp_jit_on.store(true, std::memory_order_relaxed);
+                net->grp_ct_on.store(false, std::memory_order_relaxed);
+                net->grp_quad_on.store(true, std::memory_order_relaxed);
+                HIPCHK(hipGetLastError());
+                return PCK_OK;
+            }
+        }
+        net->grp_quad_on.store(false, std::memory_order_relaxed);
         dim3 g((unsigned)((groups + per - 1) / per));
         hipFunction_t f = nullptr;
         int P = grp_p(NS);

@@ -7,7 +7,8 @@ resource-usage remarks.  No GPU needed.
 
     python tools/ct_compile_check.py [ch4|dmtm|synthetic ...] [--tables] [-DNAME=VALUE ...] [--llvm=OPT ...]
 
---tables builds the record-table kernel of the same exact size instead;
+--tables builds the record-table kernel of the same exact size instead,
+--quad the quad-group kernel (mk_quad.h);
 -D options go to hipcc (e.g. -DPCK_GRP_WAVES16=3, -DPCK_CT_CHUNK=2).
 """
 import os
@@ -43,6 +44,7 @@ def main():
     from gen_networks import emit
     global TABLES
     TABLES = '--tables' in sys.argv
+    quad = '--quad' in sys.argv            # the quad-group kernel (mk_quad.h)
     defs = [a for a in sys.argv[1:] if a.startswith('-D')]
     for a in sys.argv[1:]:                  # --llvm=OPT -> -mllvm OPT
         if a.startswith('--llvm='):
@@ -57,6 +59,12 @@ def main():
                'template __global__ void pck::k_solve_grp<%d, %d, PCK_CHK_P, false, false, %s>('
                'pck::NetView, pck::GrpView, pck::CondView, const double*, const double*, int64_t, pck::SolveArgs, '
                'pck::GrpArgs);\n' % (NS, G, 'pck::NoNet' if TABLES else 'pck::nets::Jit'))
+        if quad:
+            src = ('#define PCK_GRP_EXACT 1\n#define PCK_GRP_BAL 0\n#include "mk_solver.h"\nnamespace pck {\nnamespace nets {\n'
+                   + emit('Jit', plan) + '\n}\n}\n#include "mk_quad.h"\n'
+                   'template __global__ void pck::k_solve_q4<pck::nets::Jit>(pck::NetView, pck::CondView, const double*, '
+                   'const double*, int64_t, pck::SolveArgs, pck::GrpArgs);\n')
+        kname = 'k_solve_q4' if quad else 'k_solve_grp'
         with tempfile.TemporaryDirectory() as d:
             f = os.path.join(d, 'ct_%s.hip' % name)
             open(f, 'w').write(src)
@@ -69,12 +77,12 @@ def main():
                 print(name, 'FAILED'); print(p.stderr[-4000:]); continue
             lines = p.stderr.splitlines()
             # the remarks of the solver kernel (the header's k_drc_combine comes first)
-            start = max(i for i, l in enumerate(lines) if 'Function Name' in l and 'k_solve_grp' in l)
+            start = max(i for i, l in enumerate(lines) if 'Function Name' in l and kname in l)
             keep = [l.split('remark: ')[-1].split(' [-R')[0].strip() for l in lines[start:]
                     if re.search(r'(VGPRs:|Spill|Occupancy|ScratchSize)', l)]
             sym = subprocess.run(['/opt/rocm/lib/llvm/bin/llvm-readelf', '-s', '-W', os.path.join(d, 'k.o')],
                                  capture_output=True, text=True).stdout
-            size = [int(l.split()[2]) for l in sym.splitlines() if 'k_solve_grp' in l and 'FUNC' in l]
+            size = [int(l.split()[2]) for l in sym.splitlines() if kname in l and 'FUNC' in l]
             print('%s%s (NS=%d, R=%d, G=%d): %s; code %s bytes' % (name, ' [tables]' if TABLES else '', NS,
                                                                   len(plan.reactions), G, '; '.join(keep), size))
 
