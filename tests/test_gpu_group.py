@@ -465,12 +465,14 @@ def test_group_compile_time_network_matches_tables(P, inputs, monkeypatch, which
         net = s.device(('r5', 'r9'))
         run = lambda: s.drc_batch(('r5', 'r9'), T=np.linspace(400.0, 800.0, 64), eps=5.0e-2)
         tol = 1e-5
+    monkeypatch.setenv('PCK_GRP_QUAD', '0')
     a = run()
     assert net.group_kernel() == 2
     monkeypatch.setenv('PCK_GRP_CT', '0')
     b = run()
     assert net.group_kernel() == 1
     monkeypatch.delenv('PCK_GRP_CT')
+    monkeypatch.delenv('PCK_GRP_QUAD')
     np.testing.assert_array_equal(a['status'], b['status'])
     assert np.all(a['status'] == 0), np.unique(a['status'], return_counts=True)
     if which == 'dmtm_drc':
@@ -736,3 +738,40 @@ def test_group_screening_pass_matches_single_pass(P, inputs):
     np.testing.assert_array_equal(b['y'][:, ~ok], a['y'][:, ~ok])
     # the screened solve took fewer integrator steps (both trips counted)
     assert b['nsteps'].astype(np.int64).sum() < a['nsteps'].astype(np.int64).sum()
+
+
+@pytest.mark.parametrize('which', ['ch4', 'dmtm_drc'])
+def test_quad_group_kernel_matches_lane_group(P, inputs, monkeypatch, which):
+    """The quad-group kernel (mk_quad.h: k_solve_q4, four lanes per condition,
+    four species rows per lane, DPP broadcasts, threshold-pivoted LU) against
+    the 16-lane compile-time-network group kernel (PCK_GRP_QUAD=0): the same
+    statuses and, to rounding, the same states / TOFs / DRC coefficients.  The
+    CH4 transient (SteadyStateSolver's rtol 1e-10 / atol 1e-12) is the
+    default user of the quad kernel (R >= 2 NS); the DMTM transient DRC is
+    forced onto it (PCK_GRP_QUAD=2) to cover the DRC and retry paths."""
+    if which == 'ch4':
+        s, _ = _ch4(P, inputs)
+        net = s.device()
+        kw = dict(T=np.linspace(473.0, 573.0, 256), t0=0.0, t_end=1e4, rtol=1e-10, atol=1e-12)
+        run = lambda: s.solve_batch(**kw)
+    else:
+        s = _dmtm(P, inputs)
+        net = s.device(('r5', 'r9'))
+        run = lambda: s.drc_batch(('r5', 'r9'), T=np.linspace(400.0, 800.0, 64), eps=5.0e-2)
+    monkeypatch.setenv('PCK_GRP_QUAD', '2')
+    a = run()
+    assert net.group_kernel() == 3
+    monkeypatch.setenv('PCK_GRP_QUAD', '0')
+    b = run()
+    assert net.group_kernel() == 2
+    monkeypatch.delenv('PCK_GRP_QUAD')
+    np.testing.assert_array_equal(a['status'], b['status'])
+    assert np.all(a['status'] == 0), np.unique(a['status'], return_counts=True)
+    if which == 'ch4':
+        # measured 2.3e-12 relative above 1e-12, identical step counts
+        assert close(a['y'], b['y'], rtol=1e-9, floor=1e-14), np.abs(a['y'] - b['y']).max()
+        return
+    # transients at the input's rtol 1e-6 (measured 1.4e-6 on xi)
+    for name in s.reactions:
+        np.testing.assert_allclose(a[name], b[name], rtol=0, atol=1e-5)
+    np.testing.assert_allclose(a['tof0'], b['tof0'], rtol=1e-6)
