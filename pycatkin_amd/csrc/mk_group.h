@@ -1001,13 +1001,17 @@ __device__ __forceinline__ bool grp_lu16(const Grp<NSP>& x, LU<NSP>& F) {
             const double inv = rcp(piv);
             const bool below = x.gl > k;            // padding lanes hold zero rows: updates are no-ops
             const double l = F.W[k] * inv;
+            // the multiplier is 0 on the rows at and above k, whose trailing
+            // entries the fma then leaves as they are (one VALU op per column
+            // instead of an fma and a select)
+            const double lm = below ? -l : 0.0;
             if (x.gl == k) F.W[k] = inv;
             if (below) F.W[k] = l;
 #pragma unroll
             for (int j = k + 1; j < NSP; ++j) {
                 if (j < x.NS) {
                     const double pj = bc16(F.W[j], k);
-                    if (below) F.W[j] = fma(-l, pj, F.W[j]);
+                    F.W[j] = fma(lm, pj, F.W[j]);
                 }
             }
         }

@@ -143,6 +143,14 @@ __device__ __forceinline__ void q_rhs(const Quad& x, const double (&y)[4], doubl
 #endif
 }
 
+// some row 4 g + s (g = 0..3) has a nonzero coefficient in reaction j
+template <class Net, int j, int s>
+__device__ constexpr bool q_slot_used() {
+    for (int g = 0; g < 4; ++g)
+        if (4 * g + s < Net::NS && Net::S(4 * g + s, j) != 0.0) return true;
+    return false;
+}
+
 // the lane's 4 rows of W = ig I - J (J = d f / d y, rows scaled by rs, the
 // flow on the diagonal); padding rows (>= NS) are zero
 template <class Net>
@@ -183,8 +191,11 @@ __device__ __forceinline__ void q_jac(const Quad& x, const double (&y)[4], doubl
                     double v = 0.0;
                     if constexpr (Net::ef(j, q) > 0) v += ct_dside<Net, j, q, true>(kf, c);
                     if constexpr (Net::er(j, q) > 0) v -= ct_dside<Net, j, q, false>(kr, c);
-#pragma unroll
-                    for (int s = 0; s < 4; ++s) W[s][q] = fma(cs[s], v, W[s][q]);
+                    // only the slots some lane's row of reaction j falls in
+                    sfor<0, 4>([&](auto sc) {
+                        constexpr int s = decltype(sc)::value;
+                        if constexpr (q_slot_used<Net, j, s>()) W[s][q] = fma(cs[s], v, W[s][q]);
+                    });
                 }
             });
             if constexpr ((j + 1) % PCK_CT_CHUNK == 0) {
@@ -274,25 +285,22 @@ __device__ __forceinline__ bool q_lu(int gl, double (&W)[4][16], int (&src)[4], 
         const double akk = qb<K>(W[KR][k]);
         ok = ok && (akk != 0.0) && (akk == akk);
         const double inv = rcp1(akk);
-        // multipliers of the rows below k, then their trailing entries
-        if (gl == K) {
-            W[KR][k] = inv;
+        // multipliers of the rows below k (0 on the rows at and above it, whose
+        // trailing entries the updates then leave as they are: no exec-mask
+        // branches per column), the stored reciprocal on row k
+        double mk[4];
 #pragma unroll
-            for (int s = KR + 1; s < 4; ++s) W[s][k] *= inv;
-        } else if (gl > K) {
-#pragma unroll
-            for (int s = 0; s < 4; ++s) W[s][k] *= inv;
+        for (int s = 0; s < 4; ++s) {
+            const bool below = (gl > K) || (gl == K && s > KR);
+            const double m_s = W[s][k] * inv;
+            mk[s] = below ? -m_s : 0.0;
+            W[s][k] = below ? m_s : ((gl == K && s == KR) ? inv : W[s][k]);
         }
 #pragma unroll
         for (int j = k + 1; j < NS; ++j) {
             const double pj = qb<K>(W[KR][j]);
-            if (gl == K) {
 #pragma unroll
-                for (int s = KR + 1; s < 4; ++s) W[s][j] = fma(-W[s][k], pj, W[s][j]);
-            } else if (gl > K) {
-#pragma unroll
-                for (int s = 0; s < 4; ++s) W[s][j] = fma(-W[s][k], pj, W[s][j]);
-            }
+            for (int s = 0; s < 4; ++s) W[s][j] = fma(mk[s], pj, W[s][j]);
         }
     });
     swapped = __any(swapped);
@@ -319,31 +327,62 @@ __device__ __forceinline__ void q_solve(int gl, const double (&W)[4][16], const 
 #pragma unroll
         for (int s = 0; s < 4; ++s) b[s] = nb[s];
     }
+    // 4 x 4 blocks: the diagonal block on its own lane, then one broadcast of
+    // its 4 values and the update of the other lanes' rows -- 2 exec-mask
+    // branches and one DPP round per block instead of per column; every row
+    // still subtracts its terms in column order (the same rounding)
+    constexpr int NB = (NS + 3) / 4;
     // forward: unit lower triangle
-    sfor<0, NS - 1>([&](auto kc) {
-        constexpr int k = decltype(kc)::value;
-        constexpr int K = k / 4, KR = k % 4;
-        const double bk = qb<K>(b[KR]);
+    sfor<0, NB>([&](auto Kc) {
+        constexpr int K = decltype(Kc)::value;
         if (gl == K) {
+            sfor<1, 4>([&](auto sc) {
+                constexpr int s = decltype(sc)::value;
+                if constexpr (4 * K + s < NS) {
 #pragma unroll
-            for (int s = KR + 1; s < 4; ++s) b[s] = fma(-W[s][k], bk, b[s]);
-        } else if (gl > K) {
+                    for (int r = 0; r < s; ++r) b[s] = fma(-W[s][4 * K + r], b[r], b[s]);
+                }
+            });
+        }
+        if constexpr (K + 1 < NB) {
+            double bk[4];
 #pragma unroll
-            for (int s = 0; s < 4; ++s) b[s] = fma(-W[s][k], bk, b[s]);
+            for (int r = 0; r < 4; ++r) bk[r] = qb<K>(b[r]);
+            if (gl > K) {
+#pragma unroll
+                for (int s = 0; s < 4; ++s) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        if (4 * K + r < NS) b[s] = fma(-W[s][4 * K + r], bk[r], b[s]);
+                }
+            }
         }
     });
     // backward: U with the stored reciprocals of its diagonal
-    sfor<0, NS>([&](auto kk) {
-        constexpr int k = NS - 1 - decltype(kk)::value;
-        constexpr int K = k / 4, KR = k % 4;
-        const double xk = qb<K>(b[KR] * W[KR][k]);
+    sfor<0, NB>([&](auto Kc) {
+        constexpr int K = NB - 1 - decltype(Kc)::value;
         if (gl == K) {
-            b[KR] = xk;
+            sfor<0, 4>([&](auto rc) {
+                constexpr int r = 3 - decltype(rc)::value;
+                if constexpr (4 * K + r < NS) {
+                    b[r] = b[r] * W[r][4 * K + r];
 #pragma unroll
-            for (int s = 0; s < KR; ++s) b[s] = fma(-W[s][k], xk, b[s]);
-        } else if (gl < K) {
+                    for (int s = 0; s < r; ++s) b[s] = fma(-W[s][4 * K + r], b[r], b[s]);
+                }
+            });
+        }
+        if constexpr (K > 0) {
+            double xk[4];
 #pragma unroll
-            for (int s = 0; s < 4; ++s) b[s] = fma(-W[s][k], xk, b[s]);
+            for (int r = 0; r < 4; ++r) xk[r] = qb<K>(b[r]);
+            if (gl < K) {
+#pragma unroll
+                for (int s = 0; s < 4; ++s) {
+#pragma unroll
+                    for (int r = 3; r >= 0; --r)
+                        if (4 * K + r < NS) b[s] = fma(-W[s][4 * K + r], xk[r], b[s]);
+                }
+            }
         }
     });
 }

@@ -508,11 +508,15 @@ def test_trajectory_dense_output_vs_oracle(P, inputs, which, tmp_path):
 
 
 @pytest.mark.parametrize('which', ['cstr', 'dmtm'])
-def test_trajectory_end_not_power_of_ten(P, inputs, which):
+def test_trajectory_end_not_power_of_ten(P, inputs, which, monkeypatch):
     """times = [0, 7200]: 10**log10(7200) is one ulp above 7200, so the last
     output sample used to lie past t_end and was never written.  The last row
     of solve_odes() must be the solver's final state (the start of
-    find_steady's Newton, old_system.py:393-395) and no sample may be NaN."""
+    find_steady's Newton, old_system.py:393-395) and no sample may be NaN.
+    Trajectories run on the lane-group kernel, so the plain transient is pinned
+    to it too (PCK_GRP_QUAD=0; the quad kernel rounds differently, within the
+    transient's tolerance: test_quad_group_kernel_matches_lane_group)."""
+    monkeypatch.setenv('PCK_GRP_QUAD', '0')
     f = ('COOxReactor', 'input_Pd111.json') if which == 'cstr' else ('DMTM', 'input.json')
     s = P.read_from_input_file(os.path.join(inputs, *f))
     s.params.update(times=[0.0, 7200.0], nsteps=40)
