@@ -9,7 +9,8 @@ resource-usage remarks.  No GPU needed.
 
 --tables builds the record-table kernel of the same exact size instead,
 --quad the quad-group kernel (mk_quad.h);
--D options go to hipcc (e.g. -DPCK_GRP_WAVES16=3, -DPCK_CT_CHUNK=2).
+-D options go to hipcc (e.g. -DPCK_GRP_WAVES16=3, -DPCK_CT_CHUNK=2);
+--asm=PATH also writes the assembly (%s in PATH = the network's name).
 """
 import os
 import re
@@ -22,6 +23,7 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, 'tools'))
 INPUTS = os.path.join(ROOT, 'tests', 'golden', 'inputs')
 TABLES = False
+ASM = None
 
 
 def plan_of(name):
@@ -45,6 +47,8 @@ def main():
     global TABLES
     TABLES = '--tables' in sys.argv
     quad = '--quad' in sys.argv            # the quad-group kernel (mk_quad.h)
+    global ASM
+    ASM = next((a[len('--asm='):] for a in sys.argv[1:] if a.startswith('--asm=')), None)
     defs = [a for a in sys.argv[1:] if a.startswith('-D')]
     for a in sys.argv[1:]:                  # --llvm=OPT -> -mllvm OPT
         if a.startswith('--llvm='):
@@ -73,6 +77,9 @@ def main():
                    '-I' + os.path.join(ROOT, 'pycatkin_amd', 'csrc'), '-Rpass-analysis=kernel-resource-usage',
                    *defs, '-o', os.path.join(d, 'k.o'), f]
             p = subprocess.run(cmd, capture_output=True, text=True)
+            if ASM:                          # --asm=PATH: the kernel's assembly too
+                subprocess.run([c for c in cmd if c not in ('-c', '-Rpass-analysis=kernel-resource-usage')][:-3]
+                               + ['-S', '-o', ASM.replace('%s', name), f], capture_output=True, text=True)
             if p.returncode:
                 print(name, 'FAILED'); print(p.stderr[-4000:]); continue
             lines = p.stderr.splitlines()
