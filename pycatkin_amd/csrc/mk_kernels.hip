@@ -1205,6 +1205,12 @@ static int launch_solve(const pck_network* net, const pck_conditions* cond, cons
             pv.root_dist = a.screen_dist;
         }
         pv.max_steps = a.max_steps < 1000 ? a.max_steps : 1000;
+        {
+            // A/B: PCK_PREVIEW_MAXSTEPS, a lower cap (a capped sample counts as
+            // rejected: its wavefront goes first and skips the screening trip)
+            const char* e = getenv("PCK_PREVIEW_MAXSTEPS");
+            if (e && atoi(e) > 0) pv.max_steps = std::min(pv.max_steps, atoi(e));
+        }
         pv.y = nullptr; pv.tof = nullptr; pv.status = pscreen ? pst : nullptr; pv.nsteps = pns;
         pv.idx = list; pv.nidx = cnt; pv.retry_pass = 0; pv.worder = nullptr;
         rc = run_solver(net, cond, pv, grp, ga, traj, kf, kr, s, W * np);
