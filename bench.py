@@ -309,7 +309,8 @@ def _outputs(torch, net, n, L, _ptr):
 def _solve_workload(wl, sim, net, plan, n, T, p, desc, tof_terms, steady, activity, t_end=None, rtol=None,
                     atol=None, args=None):
     import torch
-    from pycatkin_amd.classes.system import ROOT_DIST, SCREEN_MARGIN, SCREEN_RTOL, STEADY_TRANSIENT
+    from pycatkin_amd.classes.system import (ROOT_DIST, SCREEN_MARGIN, SCREEN_MAX_LANE_SPECIES, SCREEN_RTOL,
+                                             STEADY_TRANSIENT)
     from pycatkin_amd import _lib as L
     from pycatkin_amd.engine import _ptr
     Tt, pp, d, fx, y0, inflow = sim._inputs(net, plan, n, T, p, desc, None, None, None)
@@ -327,8 +328,11 @@ def _solve_workload(wl, sim, net, plan, n, T, p, desc, tof_terms, steady, activi
                         newton=steady and not args.no_newton, newton_iters=60, activity=activity,
                         retry=tuple(args.retry) if args.retry else None,
                         root_dist=(ROOT_DIST if args.root_dist is None else args.root_dist) if steady else 0.0)
-    # the screening pass of System.solve_batch(steady=True) (SCREEN_RTOL; --screen 0: off)
-    scr = SCREEN_RTOL if getattr(args, 'screen', None) is None else args.screen
+    # the screening pass of System.solve_batch(steady=True, screen='auto'):
+    # SCREEN_RTOL on networks of at most SCREEN_MAX_LANE_SPECIES dynamic
+    # species, off beyond (--screen X forces it, --screen 0 turns it off)
+    scr = ((SCREEN_RTOL if net.NDYN <= SCREEN_MAX_LANE_SPECIES else 0.0)
+           if getattr(args, 'screen', None) is None else args.screen)
     if steady and wl.prm.newton and wl.prm.root_dist > 0.0 and not args.retry and scr > 0.0:
         wl.prm.screen_rtol, wl.prm.screen_margin = float(scr), SCREEN_MARGIN
     wl.tolerances = (wl.prm.rtol, wl.prm.atol)

@@ -968,7 +968,8 @@ struct LU {
     double W[NSP];
     Perm<NSP> pk;
     int step;
-    int src;        // 16-lane groups (physical row swaps): original row now held by this lane
+    int src;        // 16- and 64-lane groups (physical row swaps): original row now held by this lane
+    bool swp;       // 64-lane groups: some rows were interchanged (wave-uniform)
 };
 
 // 16-lane groups (one row of the wavefront per condition): LU with partial
@@ -1041,12 +1042,112 @@ __device__ __forceinline__ double grp_solve16(const Grp<NSP>& x, const LU<NSP>& 
     return x.row ? b : 0.0;
 }
 
+// 64-lane groups (one condition per wavefront; round 5): threshold pivoting
+// as the lane solver (mk_device.h: lu, PCK_PIVOT_TAU) with physical row
+// interchanges, so row k of the factors sits in lane k and every broadcast of
+// the LU and both substitutions is a v_readlane from a constant lane -- no
+// pivot-index extraction, no readfirstlane, no SGPR lane operands.  Rows are
+// interchanged only where some row below the diagonal is 1/tau times larger
+// (wave vote, rare); the pivot row is then the largest one, as in partial
+// pivoting.  The trailing update of a column runs in chunks of PCK_LU64_CHUNK
+// entries: an empty asm at each chunk boundary takes the chunk's results and
+// the next chunk's sources, so the next readlanes cannot be hoisted above the
+// chunk's FMAs (all 2 (NS - k) of them at once overflow the SGPRs and spill).
+// PCK_GRP_TPIV64=0 keeps the partial-pivoting form below.
+#ifndef PCK_GRP_TPIV64
+#define PCK_GRP_TPIV64 1
+#endif
+#ifndef PCK_LU64_CHUNK
+#define PCK_LU64_CHUNK 8
+#endif
+#ifndef PCK_LU64_TAU
+#define PCK_LU64_TAU PCK_PIVOT_TAU
+#endif
+template <int NSP>
+__device__ __forceinline__ bool grp_lu64(const Grp<NSP>& x, LU<NSP>& F) {
+    bool ok = true;
+    // the lane index through an empty asm: the per-column lane masks (gl > k,
+    // gl == k) are recomputed at each use instead of hoisted for the whole
+    // kernel into SGPR pairs that then spill (ct_row, same trick)
+    const int gl = ct_row(x.gl);
+    F.src = gl;
+    F.swp = false;
+    // the column loop by template recursion (every k a constant: LLVM's full
+    // unroll gives up on the nest and the factors go to scratch), the
+    // updates of one column by a plain unrolled loop
+    sfor<0, NSP>([&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        if (k < x.NS) {
+            const double dk = fabs(rlane(F.W[k], k)) * (1.0 / PCK_LU64_TAU);
+            if (__any(x.row && gl > k && fabs(F.W[k]) > dk)) {      // rare: wave-uniform
+                const float mag = (float)fabs(F.W[k]);
+                int key = (x.row && gl >= k) ? (int)((__float_as_uint(mag) & ~63u) | (uint32_t)gl) : -1;
+                key = gmaxi<64>(key);
+                const int p = __builtin_amdgcn_readfirstlane(key & 63);
+                if (p != k) {
+                    const int from = (gl == k) ? p : (gl == p) ? k : gl;
+#pragma unroll
+                    for (int j = 0; j < NSP; ++j) F.W[j] = __shfl(F.W[j], from, 64);
+                    F.src = __shfl(F.src, from, 64);
+                    F.swp = true;
+                }
+            }
+            const double piv = rlane(F.W[k], k);
+            ok = ok && piv != 0.0 && isfinite(piv);
+            const double inv = rcp(piv);
+            const bool below = gl > k;                 // padding lanes hold zero rows: updates are no-ops
+            const double l = F.W[k] * inv;
+            const double lm = below ? -l : 0.0;        // 0 at and above row k: the fma leaves them as they are
+            if (gl == k) F.W[k] = inv;
+            if (below) F.W[k] = l;
+#pragma unroll
+            for (int j = k + 1; j < NSP; ++j) {
+                if ((j - k - 1) % PCK_LU64_CHUNK == 0 && j > k + 1) {
+                    // chunk boundary: the previous chunk's results, then this chunk's sources
+#pragma unroll
+                    for (int q = j - PCK_LU64_CHUNK; q < j + PCK_LU64_CHUNK && q < NSP; ++q)
+                        asm volatile("" : "+v"(F.W[q]));
+                }
+                if (j < x.NS) F.W[j] = fma(lm, rlane(F.W[j], k), F.W[j]);
+            }
+        }
+    });
+    return ok;
+}
+
+template <int NSP>
+__device__ __forceinline__ double grp_solve64(const Grp<NSP>& x, const LU<NSP>& F, double b) {
+    if (F.swp) b = __shfl(b, F.src, 64);                // the row interchanges of the factorisation
+    const int gl = ct_row(x.gl);                        // see grp_lu64
+#pragma unroll
+    for (int k = 0; k < NSP; ++k) {
+        if (k < x.NS) {
+            const double bk = rlane(b, k);
+            b = fma((gl > k) ? -F.W[k] : 0.0, bk, b);
+        }
+    }
+#pragma unroll
+    for (int kk = 0; kk < NSP; ++kk) {
+        const int k = NSP - 1 - kk;
+        if (k < x.NS) {
+            const double xk = rlane(b * F.W[k], k);
+            b = fma((gl < k) ? -F.W[k] : 0.0, xk, b);
+            if (gl == k) b = xk;
+        }
+    }
+    return x.row ? b : 0.0;
+}
+
 #ifndef PCK_GRP_READLANE
 #define PCK_GRP_READLANE 1
 #endif
 template <int NSP, int G>
 __device__ __forceinline__ bool grp_lu(const Grp<NSP>& x, LU<NSP>& F) {
     if constexpr (G == 16 && NSP <= 16) return grp_lu16<NSP>(x, F);
+    // (exact-size hipRTC kernels only: the padded compiled-in fallback keeps
+    // the partial-pivoting form, whose unrolled interchanges at run-time NS
+    // took the split build's 64-lane unit past 10 minutes)
+    if constexpr (G == 64 && PCK_GRP_TPIV64 && PCK_GRP_EXACT) return grp_lu64<NSP>(x, F);
     bool fre = x.row;
     bool ok = true;
     F.step = NSP;
@@ -1107,6 +1208,7 @@ __device__ __forceinline__ bool grp_lu(const Grp<NSP>& x, LU<NSP>& F) {
 template <int NSP, int G>
 __device__ __forceinline__ double grp_solve(const Grp<NSP>& x, const LU<NSP>& F, double b) {
     if constexpr (G == 16 && NSP <= 16) return grp_solve16<NSP>(x, F, b);
+    if constexpr (G == 64 && PCK_GRP_TPIV64 && PCK_GRP_EXACT) return grp_solve64<NSP>(x, F, b);
 #pragma unroll
     for (int k = 0; k < NSP; ++k) {
         if (k < x.NS) {
@@ -1702,7 +1804,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 64
     if (!TRAJ && a.screen_rtol > 0.0) {
         y = x.row ? cv.y0[x.gl * cv.ld_y0 + c * cv.s_y0] : 0.0;
         st = grp_integrate<NSP, G, P, TRAJ, Net>(nv, gl, x, y, a.t0, a.t_end, a.screen_rtol, a.screen_atol,
-                                                 a.max_steps, ns, a.cons_rows != 0, to, F);
+                                                 a.screen_max_steps, ns, a.cons_rows != 0, to, F);
         if (st == PCK_ST_OK && a.newton)
             st = grp_newton<NSP, G, P, Net>(nv, gl, x, y, a.newton_iters, F, a.screen_dist, a.screen_atol);
         done = (st == PCK_ST_OK);

@@ -1124,6 +1124,11 @@ static int launch_solve(const pck_network* net, const pck_conditions* cond, cons
     // launches (PCK_SCREEN_INLINE=0, A/B)
     const bool screen_inline =
         screen && (grp || drc_groups || a.G != 1 || !(getenv("PCK_SCREEN_INLINE") && getenv("PCK_SCREEN_INLINE")[0] == '0'));
+    {
+        a.screen_max_steps = std::min(a.max_steps, 2000);
+        const char* e = getenv("PCK_SCREEN_MAX_STEPS");
+        if (e && atoi(e) > 0) a.screen_max_steps = std::min(a.max_steps, atoi(e));
+    }
     if (screen_inline) {
         a.screen_rtol = prm->screen_rtol;
         a.screen_atol = a.atol * (prm->screen_rtol / a.rtol);
@@ -1307,6 +1312,7 @@ static int launch_solve(const pck_network* net, const pck_conditions* cond, cons
         a1.rtol = prm->screen_rtol;
         a1.atol = a.atol * (prm->screen_rtol / a.rtol);
         a1.root_dist = a.root_dist * (prm->screen_margin > 0.0 ? prm->screen_margin : 0.1);
+        a1.max_steps = a.screen_max_steps;
         rc = run_solver(net, cond, a1, grp, ga, traj, kf, kr, s);
         if (rc) return rc;
         // pass 2: every other condition, from y0 at the caller's tolerances

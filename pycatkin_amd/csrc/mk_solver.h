@@ -1249,6 +1249,10 @@ struct SolveArgs {
     // an accepted root solves again from y0 at rtol / atol / root_dist, in
     // the same launch (screen_rtol 0: a single pass)
     double screen_rtol, screen_atol, screen_dist;
+    // the screening trip's step cap (PCK_SCREEN_MAX_STEPS, default 2000, at
+    // most max_steps): a trip past it is not accepted and the full solve runs
+    // (an optimisation never costs more than this many steps per lane)
+    int screen_max_steps;
     // cost-ordered dispatch: the first prio_waves blocks of the order (the
     // costliest wavefronts) raise their issue priority on the SIMD
     int prio_waves;
@@ -1274,7 +1278,7 @@ __device__ __forceinline__ int solve_lane(const P& p, const Lane<P::NS>& L, cons
     if (!TRAJ && a.screen_rtol > 0.0 && screen_on) {
 #pragma unroll
         for (int i = 0; i < NS; ++i) y[i] = cv.y0[i * cv.ld_y0 + c * cv.s_y0];
-        st = integrate<TRAJ>(p, L, k, y, a.t0, a.t_end, a.screen_rtol, a.screen_atol, a.max_steps, nsp,
+        st = integrate<TRAJ>(p, L, k, y, a.t0, a.t_end, a.screen_rtol, a.screen_atol, a.screen_max_steps, nsp,
                              a.cons_rows != 0, to);
         if (st == PCK_ST_OK && a.newton) st = newton(p, L, k, y, a.newton_iters, a.screen_dist, a.screen_atol);
         total = nsp;

@@ -775,3 +775,35 @@ def test_quad_group_kernel_matches_lane_group(P, inputs, monkeypatch, which):
     for name in s.reactions:
         np.testing.assert_allclose(a[name], b[name], rtol=0, atol=1e-5)
     np.testing.assert_allclose(a['tof0'], b['tof0'], rtol=1e-6)
+
+
+@pytest.mark.parametrize('n', [1, 5, 17, 33])
+def test_quad_group_kernel_ragged_batches(P, inputs, monkeypatch, n):
+    """Batches that do not fill a wavefront of 16 quads (and one condition
+    alone): the quad kernel's tail quads exit before any cross-lane step, the
+    others match the 16-lane kernel as in the full batch (CH4 transient at
+    rtol 1e-8, t_end 1e2 s; the DMTM DRC on n // 4 + 1 temperatures)."""
+    s, _ = _ch4(P, inputs)
+    net = s.device()
+    kw = dict(T=np.linspace(473.0, 573.0, n), t0=0.0, t_end=1e2, rtol=1e-8, atol=1e-12)
+    monkeypatch.setenv('PCK_GRP_QUAD', '2')
+    a = s.solve_batch(**kw)
+    assert net.group_kernel() == 3
+    monkeypatch.setenv('PCK_GRP_QUAD', '0')
+    b = s.solve_batch(**kw)
+    np.testing.assert_array_equal(a['status'], b['status'])
+    assert np.all(a['status'] == 0), _counts(a['status'])
+    assert a['y'].shape == (len(s.plan().dyn), n)
+    assert close(a['y'], b['y'], rtol=1e-7, floor=1e-14), np.abs(a['y'] - b['y']).max()
+    d = _dmtm(P, inputs)
+    m = n // 4 + 1
+    monkeypatch.setenv('PCK_GRP_QUAD', '2')
+    c = d.drc_batch(('r5', 'r9'), T=np.linspace(450.0, 750.0, m), eps=5.0e-2)
+    assert d.device(('r5', 'r9')).group_kernel() == 3
+    monkeypatch.setenv('PCK_GRP_QUAD', '0')
+    e = d.drc_batch(('r5', 'r9'), T=np.linspace(450.0, 750.0, m), eps=5.0e-2)
+    monkeypatch.delenv('PCK_GRP_QUAD')
+    np.testing.assert_array_equal(c['status'], e['status'])
+    for name in d.reactions:
+        assert c[name].shape == (m,)
+        np.testing.assert_allclose(c[name], e[name], rtol=0, atol=1e-5)

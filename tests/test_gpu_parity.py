@@ -784,3 +784,21 @@ def test_screening_pass_argument_checks(P, inputs):
     b = _screen_solve(P, inputs, 2, eco, eo, (1e-7, 0.1))
     for k in ('y', 'tof', 'status', 'nsteps'):
         np.testing.assert_array_equal(a[k], b[k])
+
+
+@pytest.mark.parametrize('cap', ['1', '40'])
+def test_screening_trip_step_cap(P, inputs, monkeypatch, cap):
+    """The screening trip stops at PCK_SCREEN_MAX_STEPS (default 2000): a
+    capped trip is not accepted and the full solve answers, so every cap gives
+    the single pass's answers (cap 1: no trip is accepted; cap 40: about half
+    the random volcano points are).  The bound keeps an explicit screen on a
+    large stiff network from costing more than the cap per condition."""
+    from pycatkin_amd.classes.system import SCREEN_MARGIN, SCREEN_RTOL
+    rng = np.random.default_rng(23)
+    n = 2048
+    eco, eo = rng.uniform(-2.5, 0.5, n), rng.uniform(-2.5, 0.5, n)
+    a = _screen_solve(P, inputs, n, eco, eo, None)
+    monkeypatch.setenv('PCK_SCREEN_MAX_STEPS', cap)
+    b = _screen_solve(P, inputs, n, eco, eo, (SCREEN_RTOL, SCREEN_MARGIN))
+    monkeypatch.delenv('PCK_SCREEN_MAX_STEPS')
+    _assert_screen_equivalent(a, b, 'cap %s' % cap)

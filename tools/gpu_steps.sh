@@ -7,7 +7,7 @@
 #   tools/gpu_steps.sh OUT STEP [STEP ...]
 #
 #   tests              pytest -m gpu (whole suite)           -> OUT/tests.log
-#   tests:EXPR         pytest -m gpu -k EXPR                 -> OUT/tests.log (appended)
+#   tests:EXPR         pytest -m gpu -k EXPR (, = space)     -> OUT/tests.log (appended)
 #   testsall[:EXPR]    the same without -x (every failure)   -> OUT/tests.log (appended)
 #   smoke              __graft_entry__.smoke()               -> OUT/smoke.log
 #   bench:ARGS         python bench.py ARGS (',' = ' ')      -> OUT/bench_<n>.json / .err
@@ -32,7 +32,7 @@ for step in "$@"; do
   echo "[gpu_steps] $(date +%T) step $k: $step" | tee -a gpurun_out/$OUT/steps.log
   case $kind in
     tests|testsall)
-      if [ -n "$arg" ]; then sel=(-k "$arg"); else sel=(); fi
+      if [ -n "$arg" ]; then sel=(-k "${arg//,/ }"); else sel=(); fi
       if [ "$kind" = tests ]; then sel+=(-x); fi
       timeout -k 10 600 python -u -m pytest tests -m gpu -q -rA --timeout 160 --timeout-method thread "${sel[@]}" \
           >> gpurun_out/$OUT/tests.log 2>&1 ;;
