@@ -1085,9 +1085,27 @@ __device__ __forceinline__ bool grp_lu64(const Grp<NSP>& x, LU<NSP>& F) {
                 key = gmaxi<64>(key);
                 const int p = __builtin_amdgcn_readfirstlane(key & 63);
                 if (p != k) {
+                    // rows k and p through LDS: row k into the concentration
+                    // buffer, row p into the pivot buffer (both free outside
+                    // the rate evaluations, which rewrite c first), then each
+                    // reads the other's -- 2 NS LDS accesses on the two lanes
+                    // instead of 2 NS ds_bpermute on the wavefront (code size:
+                    // this block is unrolled per column and per call site)
                     const int from = (gl == k) ? p : (gl == p) ? k : gl;
+                    const bool mover = (gl == k) || (gl == p);
+                    double* mine = (gl == k) ? x.c : x.pb;
+                    const double* theirs = (gl == k) ? x.pb : x.c;
+                    wsync();
+                    if (mover) {
 #pragma unroll
-                    for (int j = 0; j < NSP; ++j) F.W[j] = __shfl(F.W[j], from, 64);
+                        for (int j = 0; j < NSP; ++j) mine[j] = F.W[j];
+                    }
+                    wsync();
+                    if (mover) {
+#pragma unroll
+                        for (int j = 0; j < NSP; ++j) F.W[j] = theirs[j];
+                    }
+                    wsync();
                     F.src = __shfl(F.src, from, 64);
                     F.swp = true;
                 }
@@ -1801,7 +1819,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 64
     // is not accepted (the decision is group-uniform)
     int st = PCK_ST_NEWTON;
     bool done = false;
-    if (!TRAJ && a.screen_rtol > 0.0) {
+    // (64-lane groups run the single pass: screening is a small-network
+    // optimisation -- System.solve_batch screens networks of at most 8
+    // species -- and a second inlined integrator doubles the 64-lane kernel's
+    // code, whose unrolled LU and substitutions are most of it)
+    if (!TRAJ && G != 64 && a.screen_rtol > 0.0) {
         y = x.row ? cv.y0[x.gl * cv.ld_y0 + c * cv.s_y0] : 0.0;
         st = grp_integrate<NSP, G, P, TRAJ, Net>(nv, gl, x, y, a.t0, a.t_end, a.screen_rtol, a.screen_atol,
                                                  a.screen_max_steps, ns, a.cons_rows != 0, to, F);
