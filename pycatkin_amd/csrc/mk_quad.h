@@ -71,6 +71,24 @@ __device__ __forceinline__ double slot4(double v0, double v1, double v2, double 
 #define PCK_QUAD_ACC4 0
 #endif
 
+// the network's rows have no flow term (no CSTR in/outflow) / unit row scale
+// (no T-dependent scale): compile-time, so those per-slot registers and
+// their arithmetic fold away (DMTM, CH4)
+template <class Net>
+__device__ constexpr bool q_has_flow() {
+    for (int i = 0; i < Net::NS; ++i)
+        if (Net::dyn(i, 3) != 0.0) return true;
+    return false;
+}
+template <class Net>
+__device__ constexpr bool q_unit_rs() {
+    for (int i = 0; i < Net::NS; ++i)
+        if (Net::dyn(i, 1) != 1.0 || Net::dyn(i, 2) != 0.0) return false;
+    return true;
+}
+template <class Net>
+__device__ __forceinline__ double q_row_f(const struct Quad& x, int s, double acc, double y);
+
 // per-lane context of a quad
 struct Quad {
     int gl;                      // lane of the quad (0..3): rows 4 gl + s
@@ -79,6 +97,13 @@ struct Quad {
     const double* kr;
     double rs[4], fl[4], in[4];  // row scale, flow, inflow of the lane's rows
 };
+
+// f_i of slot s from its reaction sum: rs_i sum + fl_i (in_i - y_i)
+template <class Net>
+__device__ __forceinline__ double q_row_f(const Quad& x, int s, double acc, double y) {
+    const double r = q_unit_rs<Net>() ? acc : acc * x.rs[s];
+    return q_has_flow<Net>() ? r + x.fl[s] * (x.in[s] - y) : r;
+}
 
 // f of the lane's 4 rows: every reaction once (compile-time network), the
 // per-species sums selected for the lane's rows at the end
@@ -112,7 +137,7 @@ __device__ __forceinline__ void q_rhs(const Quad& x, const double (&y)[4], doubl
     });
     sfor<0, 4>([&](auto sc) {
         constexpr int s = decltype(sc)::value;
-        f[s] = acc[s] * x.rs[s] + x.fl[s] * (x.in[s] - y[s]);
+        f[s] = q_row_f<Net>(x, s, acc[s], y[s]);
     });
 #else
     double acc[NS];
@@ -138,7 +163,7 @@ __device__ __forceinline__ void q_rhs(const Quad& x, const double (&y)[4], doubl
             constexpr int i = 4 * g + s;
             if constexpr (i < NS) v = (gl == g) ? acc[i] : v;
         });
-        f[s] = v * x.rs[s] + x.fl[s] * (x.in[s] - y[s]);
+        f[s] = q_row_f<Net>(x, s, v, y[s]);
     });
 #endif
 }
@@ -154,7 +179,7 @@ __device__ constexpr bool q_slot_used() {
 // the lane's 4 rows of W = ig I - J (J = d f / d y, rows scaled by rs, the
 // flow on the diagonal); padding rows (>= NS) are zero
 template <class Net>
-__device__ __forceinline__ void q_jac(const Quad& x, const double (&y)[4], double ig, double (&W)[4][16]) {
+__device__ __forceinline__ void q_jac(const Quad& x, const double (&y)[4], double ig, double (&W)[4][Net::NS]) {
     constexpr int NS = Net::NS, R = Net::R;
     ct_reload();
     const int gl = ct_row(x.gl);
@@ -166,7 +191,7 @@ __device__ __forceinline__ void q_jac(const Quad& x, const double (&y)[4], doubl
 #pragma unroll
     for (int s = 0; s < 4; ++s)
 #pragma unroll
-        for (int q = 0; q < 16; ++q) W[s][q] = 0.0;
+        for (int q = 0; q < NS; ++q) W[s][q] = 0.0;
     sfor<0, R>([&](auto jc) {
         constexpr int j = decltype(jc)::value;
         if constexpr (ct_col_used<Net, j>()) {
@@ -206,11 +231,11 @@ __device__ __forceinline__ void q_jac(const Quad& x, const double (&y)[4], doubl
     });
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-        const double rs = -x.rs[s];
+        const double rs = q_unit_rs<Net>() ? -1.0 : -x.rs[s];
 #pragma unroll
-        for (int q = 0; q < 16; ++q) W[s][q] *= rs;
+        for (int q = 0; q < NS; ++q) W[s][q] *= rs;
         // the diagonal: column 4 gl + s
-        const double dg = ig + x.fl[s];
+        const double dg = q_has_flow<Net>() ? ig + x.fl[s] : ig;
 #pragma unroll
         for (int g = 0; g < 4; ++g)
             if (4 * g + s < NS) W[s][4 * g + s] += (gl == g) ? dg : 0.0;
@@ -222,7 +247,7 @@ __device__ __forceinline__ void q_jac(const Quad& x, const double (&y)[4], doubl
 // some quad of the wavefront exchanged rows (wave-uniform).  Returns false on
 // a zero or non-finite pivot.
 template <int NS>
-__device__ __forceinline__ bool q_lu(int gl, double (&W)[4][16], int (&src)[4], bool& swapped) {
+__device__ __forceinline__ bool q_lu(int gl, double (&W)[4][NS], int (&src)[4], bool& swapped) {
     bool ok = true;
     swapped = false;
 #pragma unroll
@@ -257,8 +282,8 @@ __device__ __forceinline__ bool q_lu(int gl, double (&W)[4][16], int (&src)[4], 
             swapped = true;
             const int ps = p & 3, pl = p >> 2;
 #pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                if (j < NS) {
+            for (int j = 0; j < NS; ++j) {
+                {
                     const double ak = qb<K>(W[KR][j]);
                     const double ap =
                         __shfl(slot4(W[0][j], W[1][j], W[2][j], W[3][j], ps), (int)(threadIdx.x & ~3u) | pl, 64);
@@ -309,7 +334,7 @@ __device__ __forceinline__ bool q_lu(int gl, double (&W)[4][16], int (&src)[4], 
 
 // Solve (LU) x = b for the quad; b, x: the lane's 4 rows
 template <int NS>
-__device__ __forceinline__ void q_solve(int gl, const double (&W)[4][16], const int (&src)[4], bool swapped,
+__device__ __forceinline__ void q_solve(int gl, const double (&W)[4][NS], const int (&src)[4], bool swapped,
                                         double (&b)[4]) {
     if (swapped) {                               // wave-uniform: b <- P b
         double nb[4];
@@ -473,7 +498,7 @@ __device__ __forceinline__ int q_integrate(const Quad& x, double (&y)[4], double
     }
     double t = t0;
     int blowups = 0, stall = 0;
-    double W[4][16];
+    double W[4][NS];        // the network's columns only (DMTM: 11, 40 VGPRs fewer than 16)
     int src[4];
     bool sw;
     while (t < t_end) {

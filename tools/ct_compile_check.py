@@ -86,7 +86,7 @@ def main():
             # the remarks of the solver kernel (the header's k_drc_combine comes first)
             start = max(i for i, l in enumerate(lines) if 'Function Name' in l and kname in l)
             keep = [l.split('remark: ')[-1].split(' [-R')[0].strip() for l in lines[start:]
-                    if re.search(r'(VGPRs:|Spill|Occupancy|ScratchSize)', l)]
+                    if re.search(r'(VGPRs:|AGPRs:|Spill|Occupancy|ScratchSize)', l)]
             sym = subprocess.run(['/opt/rocm/lib/llvm/bin/llvm-readelf', '-s', '-W', os.path.join(d, 'k.o')],
                                  capture_output=True, text=True).stdout
             size = [int(l.split()[2]) for l in sym.splitlines() if kname in l and 'FUNC' in l]
