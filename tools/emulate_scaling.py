@@ -50,7 +50,7 @@ def shard_ms(bench, torch, scaling, rank, world, steps, extra=()):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--steps', type=int, default=3)
-    ap.add_argument('--worlds', default='1,2,4,8', help='strong-scaling world sizes')
+    ap.add_argument('--worlds', default='1,2,4,8', help="strong-scaling world sizes (',' or '+' separated)")
     ap.add_argument('--no-weak', action='store_true')
     ap.add_argument('--bench-args', default='', help="extra bench.py arguments, '+'-separated (A/B)")
     a = ap.parse_args()
@@ -58,7 +58,7 @@ def main():
     import torch
     import bench
     out = []
-    plan = [('strong', tuple(int(w) for w in a.worlds.split(',')))] + ([] if a.no_weak else [('weak', (8,))])
+    plan = [('strong', tuple(int(w) for w in a.worlds.replace('+', ',').split(',')))] + ([] if a.no_weak else [('weak', (8,))])
     for scaling, worlds in plan:
         for N in worlds:
             ranks = [shard_ms(bench, torch, scaling, r, N, a.steps, extra) for r in range(N)]
