@@ -627,6 +627,322 @@ __device__ __forceinline__ int q_integrate(const Quad& x, double (&y)[4], double
     return PCK_ST_OK;
 }
 
+// ---------------------------------------------------------------------------
+// Newton steady-state polish on the quad (mk_group.h: grp_newton, the same
+// rules: rounding-floor and step-floor stops, linear-convergence
+// extrapolation, double-double residual refinement on the last
+// factorisation, the balance test and the steady rule against the transient
+// end).  Round 5; PCK_GRP_QUAD_NEWTON=0 keeps steady solves on the 16-lane
+// kernel.
+// ---------------------------------------------------------------------------
+
+// coefficient of row 4 gl + s in a compile-time table T(i) (0 on padding rows)
+template <class Net, int S, class F>
+__device__ __forceinline__ double q_slot_coef(int gl, F tab) {
+    double v = 0.0;
+    sfor<0, 4>([&](auto gc) {
+        constexpr int g = decltype(gc)::value;
+        if constexpr (4 * g + S < Net::NS) {
+            constexpr double t = tab(4 * g + S);
+            if constexpr (t != 0.0) v = (gl == g) ? t : v;
+        }
+    });
+    return v;
+}
+
+// f and the gross flux sum_j |S_ij| (|rf_j| + |rr_j|) of the lane's rows
+template <class Net>
+__device__ __forceinline__ void q_fgross(const Quad& x, const double (&y)[4], double (&f)[4], double (&gr)[4]) {
+    constexpr int NS = Net::NS, R = Net::R;
+    ct_reload();
+    const int gl = ct_row(x.gl);
+    double c[NS];
+    sfor<0, NS>([&](auto qc) {
+        constexpr int q = decltype(qc)::value;
+        c[q] = Net::dyn(q, 0) * qb<q / 4>(y[q % 4]);
+    });
+    double acc[4] = {0.0, 0.0, 0.0, 0.0}, gacc[4] = {0.0, 0.0, 0.0, 0.0};
+    sfor<0, R>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        if constexpr (ct_col_used<Net, j>()) {
+            double rf, rr;
+            ct_rate<Net, j>(ct_k(x.kf, j), ct_k(x.kr, j), c, rf, rr);
+            const double net = ct_sub(rf, rr), gro = fabs(rf) + fabs(rr);
+            sfor<0, 4>([&](auto sc) {
+                constexpr int s = decltype(sc)::value;
+                if constexpr (q_slot_used<Net, j, s>()) {
+                    const double v = q_slot_coef<Net, s>(gl, [](int i) constexpr { return Net::S(i, j); });
+                    acc[s] = fma(v, net, acc[s]);
+                    gacc[s] = fma(fabs(v), gro, gacc[s]);
+                }
+            });
+            ct_fence<j>(acc);
+        }
+    });
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        f[s] = q_row_f<Net>(x, s, acc[s], y[s]);
+        double g = q_unit_rs<Net>() ? gacc[s] : gacc[s] * fabs(x.rs[s]);
+        if (q_has_flow<Net>()) g += fabs(x.fl[s]) * (fabs(x.in[s]) + fabs(y[s]));
+        gr[s] = g;
+    }
+}
+
+// f of the lane's rows in double-double, rounded once (mk_group.h: ct_rhs_dd)
+template <class Net>
+__device__ __forceinline__ void q_rhs_dd(const Quad& x, const double (&y)[4], double (&f)[4]) {
+    constexpr int NS = Net::NS, R = Net::R;
+    ct_reload();
+    const int gl = ct_row(x.gl);
+    dd acc[4] = {dd_of(0.0), dd_of(0.0), dd_of(0.0), dd_of(0.0)};
+    sfor<0, R>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        if constexpr (ct_col_used<Net, j>()) {
+            double yv[4] = {y[0], y[1], y[2], y[3]};
+#pragma unroll
+            for (int s = 0; s < 4; ++s) asm volatile("" : "+v"(yv[s]));
+            dd rf = dd_of(ct_k(x.kf, j)), rr = dd_of(ct_k(x.kr, j));
+            sfor<0, NS>([&](auto ic) {
+                constexpr int i = decltype(ic)::value;
+                if constexpr (Net::ef(j, i) > 0 || Net::er(j, i) > 0) {
+                    const dd ci = two_prod(Net::dyn(i, 0), qb<i / 4>(yv[i % 4]));
+                    if constexpr (Net::ef(j, i) > 0) rf = dd_mul(rf, dd_pow(ci, Net::ef(j, i)));
+                    if constexpr (Net::er(j, i) > 0) rr = dd_mul(rr, dd_pow(ci, Net::er(j, i)));
+                }
+            });
+            const dd net = dd_add(rf, dd_neg(rr));
+            sfor<0, 4>([&](auto sc) {
+                constexpr int s = decltype(sc)::value;
+                if constexpr (q_slot_used<Net, j, s>()) {
+                    const double v = q_slot_coef<Net, s>(gl, [](int i) constexpr { return Net::S(i, j); });
+                    acc[s] = dd_add(acc[s], dd_mul(net, v));
+                }
+            });
+#pragma unroll
+            for (int s = 0; s < 4; ++s) asm volatile("" : "+v"(acc[s].hi), "+v"(acc[s].lo) :: "memory");
+        }
+    });
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        dd r = q_unit_rs<Net>() ? acc[s] : dd_mul(acc[s], x.rs[s]);
+        if (q_has_flow<Net>() && x.fl[s] != 0.0) r = dd_add(r, dd_mul(two_sum(x.in[s], -y[s]), x.fl[s]));
+        f[s] = r.hi + r.lo;
+    }
+}
+
+template <int CTRL>
+__device__ __forceinline__ dd q_dppdd(dd v) { return {dppd<CTRL>(v.hi), dppd<CTRL>(v.lo)}; }
+__device__ __forceinline__ dd q_sum_dd(dd v) {
+    v = dd_add(v, q_dppdd<0xB1>(v));
+    return dd_add(v, q_dppdd<0x4E>(v));
+}
+
+template <class Net>
+__device__ __forceinline__ int q_newton(const Quad& x, double (&y)[4], int iters, double dist, double atol) {
+    constexpr int NS = Net::NS, NC = Net::NCONS;
+    const int gl = x.gl;
+    bool real[4], pv[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        real[s] = (4 * gl + s) < NS;
+        pv[s] = false;
+    }
+    // conservation laws: the lane's coefficients, totals at the transient end,
+    // the pivot rows (compile-time rows, the lane that holds them at run time)
+    double ci[NC > 0 ? NC : 1][4], b[NC > 0 ? NC : 1];
+    sfor<0, NC>([&](auto lc) {
+        constexpr int l = decltype(lc)::value;
+        double sm = 0.0;
+        sfor<0, 4>([&](auto sc) {
+            constexpr int s = decltype(sc)::value;
+            ci[l][s] = q_slot_coef<Net, s>(gl, [](int i) constexpr { return Net::C(l, i); });
+            sm += ci[l][s] * y[s];
+        });
+        b[l] = qsum(sm);
+        constexpr int pr = Net::cpiv(l);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) pv[s] = pv[s] || (4 * gl + s == pr);
+    });
+    auto imbalance = [&](const double (&z)[4], double (&f)[4]) {
+        double gr[4];
+        q_fgross<Net>(x, z, f, gr);
+        double m = 0.0;
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+            if (real[s] && !pv[s] && f[s] != 0.0) m = fmax(m, fabs(f[s]) / gr[s]);
+        return qmax(m);
+    };
+    double z[4], zp[4], scl[4] = {1.0, 1.0, 1.0, 1.0};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) z[s] = zp[s] = y[s];
+    double bal_prev = INFINITY, prev = INFINITY, lastq = 1.0;
+    int linear = 0;
+    bool conv = false;
+    double W[4][NS];
+    int src[4];
+    bool sw = false;
+    for (int it = 0; it < iters; ++it) {
+        double Gv[4];
+        const double bal = imbalance(z, Gv);
+        if (it >= 2 && bal_prev <= PCK_BALANCE_CONV && bal > bal_prev) {
+#pragma unroll
+            for (int s = 0; s < 4; ++s) z[s] = zp[s];
+            conv = true;
+            break;
+        }
+        bal_prev = bal;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) zp[s] = z[s];
+        q_jac<Net>(x, z, 0.0, W);                     // -J
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int q = 0; q < NS; ++q) W[s][q] = -W[s][q];
+        sfor<0, NC>([&](auto lc) {
+            constexpr int l = decltype(lc)::value;
+            constexpr int pr = Net::cpiv(l);
+            double sm = 0.0;
+#pragma unroll
+            for (int s = 0; s < 4; ++s) sm += ci[l][s] * z[s];
+            sm = qsum(sm);
+            if (gl == pr / 4) {
+                Gv[pr % 4] = sm - b[l];
+                sfor<0, NS>([&](auto qc) {
+                    constexpr int q = decltype(qc)::value;
+                    W[pr % 4][q] = Net::C(l, q);
+                });
+            }
+        });
+        // row equilibration (rate rows up to 1e9, conservation rows O(1))
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            double m = 0.0;
+#pragma unroll
+            for (int q = 0; q < NS; ++q) m = fmax(m, fabs(W[s][q]));
+            scl[s] = (m > 0.0) ? 1.0 / m : 1.0;
+#pragma unroll
+            for (int q = 0; q < NS; ++q) W[s][q] *= scl[s];
+            Gv[s] = -Gv[s] * scl[s];
+        }
+        if (!q_lu<NS>(gl, W, src, sw)) break;
+        q_solve<NS>(gl, W, src, sw, Gv);              // Gv <- dz
+        double alpha = 1.0;
+        if (linear >= 2 && lastq < 0.9) {
+            alpha = fmin(4.0, 1.0 / (1.0 - lastq));
+            double cand = INFINITY;
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+                if (real[s] && Gv[s] < 0.0 && z[s] > 0.0) cand = fmin(cand, 0.9 * z[s] / -Gv[s]);
+            alpha = fmax(fmin(alpha, qmin(cand)), 1.0);
+        }
+        bool fin = true;
+        double zmax = 0.0;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            Gv[s] *= alpha;
+            z[s] += Gv[s];
+            if (real[s]) {
+                fin = fin && isfinite(z[s]);
+                zmax = fmax(zmax, fabs(z[s]));
+            }
+        }
+        if (!(qmin(fin ? 1.0 : 0.0) > 0.0)) break;
+        zmax = qmax(zmax);
+        double rl = 0.0;
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+            if (real[s]) rl = fmax(rl, fabs(Gv[s]) / fmax(fabs(z[s]), 1e-12 * zmax + 1e-300));
+        const double rel = qmax(rl);
+        if (prev < PCK_STEP_FLOOR && rel > prev) {     // mk_solver.h: the step floor
+#pragma unroll
+            for (int s = 0; s < 4; ++s) z[s] = zp[s];
+            conv = true;
+            break;
+        }
+        if (rel < 1e-12 || (it >= 2 && rel < 1e-7 && rel > 0.5 * prev)) { conv = true; break; }
+        lastq = rel / prev;
+        linear = (rel > 0.25 * prev) ? linear + 1 : 0;
+        if (linear >= 12) break;
+        prev = rel;
+    }
+    if (!conv) return PCK_ST_NEWTON;
+    if (PCK_NEWTON_REFINE > 0) {
+        // residual refinement on the loop's last factorisation and row scale
+        double nprev = INFINITY, zq[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) zq[s] = z[s];
+#pragma unroll 1
+        for (int r = 0; r <= PCK_NEWTON_REFINE; ++r) {
+            double Gv[4];
+            q_rhs_dd<Net>(x, z, Gv);
+            sfor<0, NC>([&](auto lc) {
+                constexpr int l = decltype(lc)::value;
+                constexpr int pr = Net::cpiv(l);
+                dd sm = dd_of(0.0);
+#pragma unroll
+                for (int s = 0; s < 4; ++s) sm = dd_add(sm, two_prod(ci[l][s], z[s]));
+                const dd t = dd_add(q_sum_dd(sm), dd_of(-b[l]));
+                if (gl == pr / 4) Gv[pr % 4] = t.hi + t.lo;
+            });
+            double nr = 0.0;
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                Gv[s] = -Gv[s] * scl[s];
+                if (real[s]) nr = fmax(nr, fabs(Gv[s]));
+            }
+            nr = qmax(nr);
+            if (!(nr < nprev)) {                        // no longer falling: the previous iterate
+                if (r > 0) {
+#pragma unroll
+                    for (int s = 0; s < 4; ++s) z[s] = zq[s];
+                }
+                break;
+            }
+            nprev = nr;
+            if (r == PCK_NEWTON_REFINE || nr == 0.0) break;
+            q_solve<NS>(gl, W, src, sw, Gv);
+            double zmax = 0.0;
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+                if (real[s]) zmax = fmax(zmax, fabs(z[s]));
+            zmax = qmax(zmax);
+            double rl = 0.0;
+            bool fin = true;
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                if (real[s]) rl = fmax(rl, fabs(Gv[s]) / fmax(fabs(z[s]), 1e-12 * zmax + 1e-300));
+                zq[s] = z[s];
+                z[s] += Gv[s];
+                if (real[s]) fin = fin && isfinite(z[s]);
+            }
+            const double rel = qmax(rl);
+            if (!(qmin(fin ? 1.0 : 0.0) > 0.0) || !(rel <= PCK_REFINE_MAXSTEP)) {
+#pragma unroll
+                for (int s = 0; s < 4; ++s) z[s] = zq[s];
+                break;
+            }
+        }
+    }
+    bool neg = false, far = false;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        if (real[s]) {
+            neg = neg || z[s] < 0.0;
+            far = far || !(fabs(z[s] - y[s]) <= dist * fabs(z[s]) + atol);
+        }
+    }
+    if (qmax(neg ? 1.0 : 0.0) > 0.0) return PCK_ST_NEWTON;
+    {
+        double f[4];
+        if (!(imbalance(z, f) <= PCK_BALANCE_TOL)) return PCK_ST_NEWTON;   // converged in absolute terms only
+    }
+    // mk_solver.h: newton -- the root only if the transient end reached it
+    if (dist > 0.0 && qmax(far ? 1.0 : 0.0) > 0.0) return PCK_ST_NEWTON;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) y[s] = real[s] ? z[s] : 0.0;
+    return PCK_ST_OK;
+}
+
 // TOF of the quad's state (old_system.py:482-488): the listed reactions'
 // net rates, every lane the same value
 template <class Net>
@@ -656,7 +972,7 @@ __device__ __forceinline__ double q_tof(const NetView& nv, const Quad& x, const 
 #define PCK_QUAD_WAVES 1
 #endif
 // one condition (or one DRC perturbation of one) per quad; 16 per block
-template <class Net>
+template <class Net, bool NEWTON = false>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PCK_QUAD_WAVES))) k_solve_q4(NetView nv, CondView cv, const double* kf, const double* kr,
                                                  int64_t ld_k, SolveArgs a, GrpArgs ga) {
     static_assert(Net::NS <= 16, "quad-group solver: at most 16 dynamic species");
@@ -709,7 +1025,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PCK_QUA
     }
     wsync();
     int ns = 0;
+    // (a screening pass is not run here: System.solve_batch screens networks
+    // of at most 8 species, all of them on the lane solver; a single pass
+    // gives the same answers)
     int st = q_integrate<Net>(x, y, a.t0, a.t_end, a.rtol, a.atol, a.max_steps, ns);
+    if constexpr (NEWTON) {
+        if (st == PCK_ST_OK && a.newton) st = q_newton<Net>(x, y, a.newton_iters, a.root_dist, a.atol);
+    }
     const double tof = q_tof<Net>(nv, x, y);
     bool fin = isfinite(tof);
 #pragma unroll

@@ -717,14 +717,17 @@ def test_balanced_walk_matches_row_loops(P, inputs, synthetic, monkeypatch):
     assert close(a['y'], b['y'], rtol=1e-7, floor=1e-13), np.abs(a['y'] - b['y']).max()
 
 
-def test_group_screening_pass_matches_single_pass(P, inputs):
+def test_group_screening_pass_matches_single_pass(P, inputs, monkeypatch):
     """The screening pass on the lane-group kernel (System.solve_batch with
     screen=rtol; 'auto' screens one-lane networks only): DMTM steady states
     over a T x p grid -- the rule at rtol 1e-2 first, the full solve where it
     is not accepted (group-uniform) -- report what the single pass reports:
     the same statuses, the same roots to the refinement's rounding, the same
-    transient ends bitwise (mk_group.h: k_solve_grp)."""
+    transient ends bitwise (mk_group.h: k_solve_grp).  The quad kernel,
+    which runs these steady solves by default, does not screen (a single
+    pass), so the 16-lane kernel is pinned here (PCK_GRP_QUAD_NEWTON=0)."""
     from pycatkin_amd.classes.system import SCREEN_RTOL
+    monkeypatch.setenv('PCK_GRP_QUAD_NEWTON', '0')
     s = _dmtm(P, inputs)
     TT, pp = np.meshgrid(np.linspace(450.0, 750.0, 8), np.logspace(4.0, 6.0, 8), indexing='ij')
     kw = dict(T=TT.ravel(), p=pp.ravel(), steady=True)
@@ -807,3 +810,27 @@ def test_quad_group_kernel_ragged_batches(P, inputs, monkeypatch, n):
     for name in d.reactions:
         assert c[name].shape == (m,)
         np.testing.assert_allclose(c[name], e[name], rtol=0, atol=1e-5)
+
+
+def test_quad_newton_matches_lane_group_steady(P, inputs, monkeypatch):
+    """Steady solves on the quad-group kernel (mk_quad.h: q_newton, the
+    Newton polish with the refinement, balance test and steady rule of
+    mk_group.h: grp_newton) against the 16-lane kernel
+    (PCK_GRP_QUAD_NEWTON=0): DMTM steady states over a T x p grid -- the same
+    statuses, the same roots to the refinement's rounding, the same TOFs."""
+    s = _dmtm(P, inputs)
+    net = s.device(('r5', 'r9'))
+    TT, pp = np.meshgrid(np.linspace(450.0, 750.0, 16), np.logspace(4.0, 6.0, 16), indexing='ij')
+    kw = dict(T=TT.ravel(), p=pp.ravel(), tof_terms=('r5', 'r9'), steady=True)
+    a = s.solve_batch(**kw)
+    assert net.group_kernel() == 3
+    monkeypatch.setenv('PCK_GRP_QUAD_NEWTON', '0')
+    b = s.solve_batch(**kw)
+    assert net.group_kernel() == 2
+    monkeypatch.delenv('PCK_GRP_QUAD_NEWTON')
+    pairs = _counts(np.array(['%d->%d' % (u, v) for u, v in zip(b['status'], a['status'])]))
+    assert np.array_equal(a['status'], b['status']), pairs
+    ok = a['status'] == 0
+    assert ok.mean() > 0.5, pairs
+    assert close(a['y'][:, ok], b['y'][:, ok], rtol=1e-8, floor=1e-14), np.abs(a['y'] - b['y']).max()
+    np.testing.assert_allclose(a['tof'][ok], b['tof'][ok], rtol=1e-8)
