@@ -950,11 +950,11 @@ static int run_solver(const pck_network* net, const pck_conditions* cond, const 
         // solves of networks of at most 16 species: the quad-group kernel
         // (mk_quad.h), four lanes per condition (steady solves with its Newton
         // polish unless PCK_GRP_QUAD_NEWTON=0)
-        if (NS <= 16 && !traj && (!a.newton || grp_quad_newton_enabled()) && !a.cons_rows &&
+        if (NS <= 16 && (!a.newton || grp_quad_newton_enabled()) && !a.cons_rows &&
             net->plan_mode != PCK_PLAN_RUNTIME && jit_enabled() &&
             grp_quad_enabled(NS, net->nv.NRXN) && grp_ct_enabled(G, net->nv.NRXN) && !net->jit_grp_src.empty()) {
             hipFunction_t fq =
-                jit_group_quad_kernel(net->digest, net->jit_grp_src, net->grp_npmax, net->grp_emax, a.newton != 0);
+                jit_group_quad_kernel(net->digest, net->jit_grp_src, net->grp_npmax, net->grp_emax, a.newton != 0, traj);
             if (fq) {
                 const int R1 = net->nv.NRXN > 0 ? net->nv.NRXN : 1;
                 const size_t shm = sizeof(double) * 16 * 2 * (size_t)R1;

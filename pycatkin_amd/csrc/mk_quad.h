@@ -413,9 +413,9 @@ __device__ __forceinline__ void q_solve(int gl, const double (&W)[4][NS], const 
 }
 
 // RODAS4P on the quad (mk_group.h: grp_integrate, transient only)
-template <class Net>
+template <class Net, bool TRAJ = false>
 __device__ __forceinline__ int q_integrate(const Quad& x, double (&y)[4], double t0, double t_end, double rtol,
-                                           double atol, int max_steps, int& nsteps) {
+                                           double atol, int max_steps, int& nsteps, const TrajOut& to = TrajOut{}) {
     using namespace rodas4;
     constexpr int NS = Net::NS;
     constexpr int NC = Net::NCONS;
@@ -423,10 +423,26 @@ __device__ __forceinline__ int q_integrate(const Quad& x, double (&y)[4], double
     bool real[4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) real[s] = (4 * gl + s) < NS;
+    // trajectory samples (mk_group.h: grp_integrate): the lane's rows of
+    // sample k at to.y[(k NS + i) ld + c]
+    int ko = 0;
+    auto put = [&](int k, const double (&v)[4]) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+            if (real[s]) to.y[((int64_t)k * NS + 4 * gl + s) * to.ld + to.c] = v[s];
+    };
+    if constexpr (TRAJ) {
+        for (; ko < to.n && to.t[ko] <= t0; ++ko) put(ko, y);
+    }
     const double invNS = 1.0 / NS;
     nsteps = 0;
     const double span = t_end - t0;
-    if (!(span > 0.0)) return PCK_ST_OK;
+    if (!(span > 0.0)) {
+        if constexpr (TRAJ) {
+            for (; ko < to.n; ++ko) put(ko, y);
+        }
+        return PCK_ST_OK;
+    }
     double F0[4];
     q_rhs<Net>(x, y, F0);
     // conservation laws: the lane's coefficients (small integers: exact in
@@ -559,6 +575,15 @@ __device__ __forceinline__ int q_integrate(const Quad& x, double (&y)[4], double
         for (int s = 0; s < 4; ++s) k5[s] = fu[s] + ih * (C51 * k1[s] + C52 * k2[s] + C53 * k3[s] + C54 * k4[s]);
         q_solve<NS>(gl, W, src, sw, k5);
         kproj(k5);
+        double d2[TRAJ ? 4 : 1], d3[TRAJ ? 4 : 1];     // dense output (mk_solver.h: rodas4_dense)
+        if constexpr (TRAJ) {
+            using namespace rodas4_dense;
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                d2[s] = D21 * k1[s] + D22 * k2[s] + D23 * k3[s] + D24 * k4[s] + D25 * k5[s];
+                d3[s] = D3_K5_ONLY ? D35 * k5[s] : D31 * k1[s] + D32 * k2[s] + D33 * k3[s] + D34 * k4[s] + D35 * k5[s];
+            }
+        }
 #pragma unroll
         for (int s = 0; s < 4; ++s) u[s] += k5[s];
         q_rhs<Net>(x, u, fu);
@@ -585,6 +610,12 @@ __device__ __forceinline__ int q_integrate(const Quad& x, double (&y)[4], double
         const double pf = PCK_POSITIVITY ? qmin(pfl) : 1.0;
         const double fac = step_factor(q);
         if (q <= 1.0 && pf >= 1.0) {
+            const double t_old = t;
+            double y_old[TRAJ ? 4 : 1];
+            if constexpr (TRAJ) {
+#pragma unroll
+                for (int s = 0; s < 4; ++s) y_old[s] = y[s];
+            }
             t = last ? t_end : t + h;
 #pragma unroll
             for (int s = 0; s < 4; ++s) y[s] = real[s] ? u[s] : 0.0;
@@ -601,6 +632,16 @@ __device__ __forceinline__ int q_integrate(const Quad& x, double (&y)[4], double
                         if (ci[l][s] != 0.0f) y[s] *= fct;
                 }
             });
+            if constexpr (TRAJ) {
+                // samples inside (t_old, t]: the dense output of this step
+                for (; ko < to.n && to.t[ko] <= t; ++ko) {
+                    const double sv = fmin((to.t[ko] - t_old) / h, 1.0), s1 = 1.0 - sv;
+                    double v[4];
+#pragma unroll
+                    for (int s = 0; s < 4; ++s) v[s] = y_old[s] * s1 + sv * (y[s] + s1 * (d2[s] + sv * d3[s]));
+                    put(ko, v);
+                }
+            }
             q_rhs<Net>(x, y, F0);
             // falling tolerance-level negatives to 0 (mk_solver.h: integrate)
             bool negf = false;
@@ -623,6 +664,10 @@ __device__ __forceinline__ int q_integrate(const Quad& x, double (&y)[4], double
         stall = (h < PCK_STALL_H * (t - t0)) ? stall + 1 : 0;
         if (stall > PCK_STALL_STEPS) return PCK_ST_STEPFAIL;
         if (!(h > 2.220446049250313e-15 * fmax(fabs(t), 1e-300)) && t < t_end) return PCK_ST_STEPFAIL;
+    }
+    if constexpr (TRAJ) {
+        // samples past t_end (a log grid can round one ulp above it): the final state
+        for (; ko < to.n; ++ko) put(ko, y);
     }
     return PCK_ST_OK;
 }
@@ -972,7 +1017,7 @@ __device__ __forceinline__ double q_tof(const NetView& nv, const Quad& x, const 
 #define PCK_QUAD_WAVES 1
 #endif
 // one condition (or one DRC perturbation of one) per quad; 16 per block
-template <class Net, bool NEWTON = false>
+template <class Net, bool NEWTON = false, bool TRAJ = false>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PCK_QUAD_WAVES))) k_solve_q4(NetView nv, CondView cv, const double* kf, const double* kr,
                                                  int64_t ld_k, SolveArgs a, GrpArgs ga) {
     static_assert(Net::NS <= 16, "quad-group solver: at most 16 dynamic species");
@@ -1028,7 +1073,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PCK_QUA
     // (a screening pass is not run here: System.solve_batch screens networks
     // of at most 8 species, all of them on the lane solver; a single pass
     // gives the same answers)
-    int st = q_integrate<Net>(x, y, a.t0, a.t_end, a.rtol, a.atol, a.max_steps, ns);
+    const TrajOut to{a.t_out, a.n_out, a.traj, a.ld_traj, c};
+    int st = q_integrate<Net, TRAJ>(x, y, a.t0, a.t_end, a.rtol, a.atol, a.max_steps, ns, to);
     if constexpr (NEWTON) {
         if (st == PCK_ST_OK && a.newton) st = q_newton<Net>(x, y, a.newton_iters, a.root_dist, a.atol);
     }

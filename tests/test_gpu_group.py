@@ -834,3 +834,23 @@ def test_quad_newton_matches_lane_group_steady(P, inputs, monkeypatch):
     assert ok.mean() > 0.5, pairs
     assert close(a['y'][:, ok], b['y'][:, ok], rtol=1e-8, floor=1e-14), np.abs(a['y'] - b['y']).max()
     np.testing.assert_allclose(a['tof'][ok], b['tof'][ok], rtol=1e-8)
+
+
+def test_quad_trajectories_match_lane_group(P, inputs, monkeypatch):
+    """Trajectory samples (System.solve_odes / solve_batch(t_out=...)) from
+    the quad kernel's dense output against the 16-lane kernel's
+    (PCK_GRP_QUAD=0): DMTM over 32 temperatures, 41 log-spaced samples from
+    0 to 1e4 s (and one sample past t_end by rounding) at rtol 1e-10."""
+    s = _dmtm(P, inputs)
+    net = s.device()
+    t_out = np.concatenate([[0.0], np.logspace(-8.0, 4.0, 40), [1e4 * (1.0 + 4e-16)]])
+    kw = dict(T=np.linspace(450.0, 750.0, 32), t0=0.0, t_end=1e4, rtol=1e-10, atol=1e-14, t_out=t_out)
+    a = s.solve_batch(**kw)
+    assert net.group_kernel() == 3
+    monkeypatch.setenv('PCK_GRP_QUAD', '0')
+    b = s.solve_batch(**kw)
+    monkeypatch.delenv('PCK_GRP_QUAD')
+    np.testing.assert_array_equal(a['status'], b['status'])
+    assert np.all(np.isfinite(a['traj']))
+    assert close(a['traj'], b['traj'], rtol=1e-6, floor=1e-12), np.abs(a['traj'] - b['traj']).max()
+    np.testing.assert_allclose(a['traj'][-1], a['y'], rtol=1e-12, atol=1e-300)

@@ -66,8 +66,9 @@ def main():
         if quad:
             src = ('#define PCK_GRP_EXACT 1\n#define PCK_GRP_BAL 0\n#include "mk_solver.h"\nnamespace pck {\nnamespace nets {\n'
                    + emit('Jit', plan) + '\n}\n}\n#include "mk_quad.h"\n'
-                   'template __global__ void pck::k_solve_q4<pck::nets::Jit, %s>(pck::NetView, pck::CondView, const double*, '
-                   'const double*, int64_t, pck::SolveArgs, pck::GrpArgs);\n' % ('true' if '--newton' in sys.argv else 'false'))
+                   'template __global__ void pck::k_solve_q4<pck::nets::Jit, %s, %s>(pck::NetView, pck::CondView, '
+                   'const double*, const double*, int64_t, pck::SolveArgs, pck::GrpArgs);\n'
+                   % ('true' if '--newton' in sys.argv else 'false', 'true' if '--traj' in sys.argv else 'false'))
         kname = 'k_solve_q4' if quad else 'k_solve_grp'
         with tempfile.TemporaryDirectory() as d:
             f = os.path.join(d, 'ct_%s.hip' % name)
