@@ -1063,6 +1063,9 @@ __device__ __forceinline__ double grp_solve16(const Grp<NSP>& x, const LU<NSP>& 
 #ifndef PCK_LU64_TAU
 #define PCK_LU64_TAU PCK_PIVOT_TAU
 #endif
+#ifndef PCK_SOLVE64_BRANCH
+#define PCK_SOLVE64_BRANCH 0
+#endif
 template <int NSP>
 __device__ __forceinline__ bool grp_lu64(const Grp<NSP>& x, LU<NSP>& F) {
     bool ok = true;
@@ -1141,7 +1144,11 @@ __device__ __forceinline__ double grp_solve64(const Grp<NSP>& x, const LU<NSP>& 
     for (int k = 0; k < NSP; ++k) {
         if (k < x.NS) {
             const double bk = rlane(b, k);
+#if PCK_SOLVE64_BRANCH
+            if (gl > k) b = fma(-F.W[k], bk, b);        // A/B: exec-mask branch instead of a select
+#else
             b = fma((gl > k) ? -F.W[k] : 0.0, bk, b);
+#endif
         }
     }
 #pragma unroll
@@ -1149,7 +1156,11 @@ __device__ __forceinline__ double grp_solve64(const Grp<NSP>& x, const LU<NSP>& 
         const int k = NSP - 1 - kk;
         if (k < x.NS) {
             const double xk = rlane(b * F.W[k], k);
+#if PCK_SOLVE64_BRANCH
+            if (gl < k) b = fma(-F.W[k], xk, b);
+#else
             b = fma((gl < k) ? -F.W[k] : 0.0, xk, b);
+#endif
             if (gl == k) b = xk;
         }
     }
