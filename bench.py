@@ -171,8 +171,9 @@ BOX_CPU_SHARE = 16
 # which reference path the CPU baseline's oracle call restates, per config
 CPU_PATH = dict(
     volcano='System.solve_odes with ode_solver "ode" (lsoda, the input\'s rtol 1e-8 / atol 1e-10) then the Newton '
-            'polish of find_steady (old_system.py:315-468), i.e. activity(ss_solve=True) after a transient; the '
-            'reference\'s own activity() runs at 0.79x this port per core (profiles/r3/cpu_reference_vs_port.json)',
+            'polish of find_steady (old_system.py:315-468), i.e. activity(ss_solve=True) after a transient; this '
+            'port runs at 0.785x the reference\'s own activity() per core (7.22 vs 9.20 solves/s, '
+            'profiles/r3/cpu_reference_vs_port.json), so the reference itself would do ~1.27x this value',
     cstr='System.solve_odes (lsoda) + find_steady on the Pd111 CSTR (presets.run_temperatures, '
          'steady_state_solve=True)',
     dmtm_drc='System.degree_of_rate_control (2R+1 transients, old_system.py:490-515)',
@@ -340,9 +341,8 @@ def _solve_workload(wl, sim, net, plan, n, T, p, desc, tof_terms, steady, activi
     # solver launches per step: the first pass, the degenerate-root retry and,
     # on the lane solver with cost-ordered dispatch, its preview
     ordered = net.NDYN <= 8 and (wl.prm.wave_order == 1 or (wl.prm.wave_order == 0 and n >= 262144))
-    # (the screening pass is a second launch only with PCK_SCREEN_INLINE=0)
-    screened = net.NDYN <= 8 and wl.prm.screen_rtol > 0.0 and os.environ.get('PCK_SCREEN_INLINE', '1') == '0'
-    wl.solver_launches = 1 + int(bool(wl.prm.newton and wl.prm.retry_rtol > 0.0)) + int(ordered) + int(screened)
+    # (the screening pass runs inside the first pass's launch)
+    wl.solver_launches = 1 + int(bool(wl.prm.newton and wl.prm.retry_rtol > 0.0)) + int(ordered)
     wl.out, wl.o = _outputs(torch, net, n, L, _ptr)
     wl.kf = torch.empty((max(net.NRXN, 1), max(n, 1)), dtype=torch.float64, device='cuda')
     wl.kr = torch.empty_like(wl.kf)
@@ -481,7 +481,7 @@ def synthetic_workload(args, rank, world):
     # transient (profiles/r4/synthetic_tol_probe.jsonl)
     _solve_workload(wl, sim, net, plan, n, np.full(n, 500.0), None, {'D%d' % k: D[:, k] for k in range(4)},
                     ('R0',), True, False, rtol=SYNTHETIC_TOL[0], atol=SYNTHETIC_TOL[1], args=args)
-    wl.kernel_name = 'k_solve_grp<64, 64>'
+    wl.kernel_name = 'k_solve_grp<50, 64>'
     wl.tag = 'synthetic %d' % n_tot
     wl.config = {'workload': 'synthetic 50 species / 150 reactions, %d random-descriptor conditions, T=500 K, '
                              'transient to t_end 1e4 s at rtol %g / atol %g + Newton, steady rule (root where '
@@ -744,8 +744,8 @@ def main(argv=None):
                                     'WRITE_SIZE, per-launch average x solver launches per step)',
                     'traffic_source': traffic_src, 'algorithmic_bytes': wl.algo_bytes,
                     'kernel': wl.kernel_name, 'kernel_ms': k3_ms, 'rate_constants_ms': k1_ms,
-                    'flops_per_launch': fl, 'flops_structural': fl_struct, 'flops_pmc_f64': fl_pmc,
-                    'flops_per_step': fps, 'flop_count': 'min(structural nonzeros of one accepted RODAS4P step x '
+                    'flops_per_bench_step': fl, 'flops_structural': fl_struct, 'flops_pmc_f64': fl_pmc,
+                    'flops_per_integrator_step': fps, 'flop_count': 'min(structural nonzeros of one accepted RODAS4P step x '
                     'integrator steps of rank 0 (every solver pass: screening + full, or first pass + retry; the preview, Newton polish, kernel 1 and TOF not counted), '
                     '64 x (ADD+MUL+TRANS) + 128 x FMA fp64 wave instructions of the committed PMC profile of this '
                     'workload, per launch x solver launches per step)',

@@ -163,16 +163,19 @@ typedef struct {
                             *   PCK_ST_NEWTON (old_system.py:517-529 System.activity semantics).
                             *   0: any converged, balanced, non-negative root is reported
                             *   (old_system.py:385-468 find_steady from a given state). */
-    double screen_rtol;    /* with newton and root_dist > 0 (pck_solve on the one-lane path, no
-                            *   trajectory, no retry_rtol): a screening pass at rtol = screen_rtol
-                            *   (atol scaled alike) whose Newton root is accepted (PCK_ST_OK) only if
-                            *   the screening transient's end lies within screen_margin * root_dist
-                            *   of it; every other condition is then solved again from y0 at
-                            *   rtol / atol by a second launch over their compacted list, exactly
-                            *   as without screening (y, tof, status of that solve; nsteps adds the
-                            *   two passes).  A transient that has settled on a root ends on it
-                            *   at any tolerance, so the accepted conditions report the root the
-                            *   single pass would (DESIGN.md "Screening pass").  0: off. */
+    double screen_rtol;    /* with newton and root_dist > 0 (no trajectory): a screening pass at
+                            *   rtol = screen_rtol (atol scaled alike) whose Newton root is accepted
+                            *   (PCK_ST_OK) only if the screening transient's end lies within
+                            *   screen_margin * root_dist * |root_i| + atol (the caller's atol) of
+                            *   it; every other condition solves again from y0 at rtol / atol in the
+                            *   same launch, exactly as without screening (y, tof, status of that
+                            *   solve; nsteps adds the two trips).  A transient that has settled on
+                            *   a root ends on it at any tolerance, so the accepted conditions report
+                            *   the root the single pass would (DESIGN.md "Screening pass").  Runs on
+                            *   the one-lane solver and the 16- and 32-lane group kernels, pck_solve
+                            *   and pck_drc; a network of <= 16 species then leaves the quad-group
+                            *   kernel for the 16-lane one; networks of > 32 species (64-lane
+                            *   groups) refuse it with PCK_E_ARG.  0: off. */
     double screen_margin;  /*   fraction of root_dist for the screening pass's acceptance (0: 0.1) */
 } pck_solve_params;
 
@@ -224,6 +227,11 @@ int pck_network_destroy(pck_network* net);
  * tables, 2 hipRTC with the network compiled in (PCK_GRP_CT=0 disables it). */
 #define PCK_PLAN_ID_JIT 100
 int pck_network_dims(const pck_network* net, int32_t* dims);
+/* Lanes per condition of the last lane-group solve (networks beyond the
+ * one-lane limits): 4 for the quad-group kernel (csrc/mk_quad.h, <= 16
+ * species), else the group width G = 16, 32 or 64 (csrc/mk_group.h: grp_g);
+ * 0 before any group solve.  Diagnostic: which kernel answered. */
+int pck_network_group_lanes(const pck_network* net, int32_t* lanes);
 /* Solver selection (A/B checks): PCK_PLAN_AUTO (default: compiled-in plan when
  * the structural digest matches, else the runtime plan, lane-group solver
  * beyond the one-lane limits), PCK_PLAN_RUNTIME (never the compiled-in plan),

@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get('PCK_LIB') or os.path.join(_HERE, 'libpycatkin_amd.so'
 
 # symbols declared in include/pycatkin_amd.h (checked by tests/test_capi.py)
 EXPORTED = ('pck_abi_version', 'pck_last_error', 'pck_network_create', 'pck_network_destroy',
-            'pck_network_dims', 'pck_network_set_plan_mode', 'pck_energies', 'pck_rate_constants', 'pck_species_rates',
+            'pck_network_dims', 'pck_network_group_lanes', 'pck_network_set_plan_mode', 'pck_energies', 'pck_rate_constants', 'pck_species_rates',
             'pck_reaction_rates', 'pck_jacobian', 'pck_solve', 'pck_drc')
 
 ABI_VERSION = 6
@@ -82,6 +82,7 @@ def load():
     lib.pck_network_create.argtypes = [vp, i64, vp, i64, C.POINTER(vp)]
     lib.pck_network_destroy.argtypes = [vp]
     lib.pck_network_dims.argtypes = [vp, i32p]
+    lib.pck_network_group_lanes.argtypes = [vp, i32p]
     lib.pck_network_set_plan_mode.argtypes = [vp, C.c_int]
     lib.pck_energies.argtypes = [vp, C.POINTER(Conditions), vp, i64, vp]
     lib.pck_rate_constants.argtypes = [vp, C.POINTER(Conditions), vp, vp, i64, vp]

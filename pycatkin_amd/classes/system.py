@@ -478,7 +478,9 @@ class System:
         and no t_out; None: off; a number: the screening rtol) runs the rule
         at that loose tolerance first and solves only the conditions it does
         not accept at the transient tolerances ('auto' on one-lane networks
-        only; a number screens lane-group networks too)."""
+        only; a number screens the 16- / 32-lane group networks too, a network
+        of at most 16 species then running on the 16-lane kernel instead of
+        the quad one; networks of more than 32 species refuse it)."""
         plan = self.plan(tuple(tof_terms), None)
         net = self.device(tuple(tof_terms), None)
         sizes = [T, p] + (list(desc.values()) if desc else [])

@@ -45,6 +45,7 @@ struct pck_network {
     mutable std::atomic<bool> grp_jit_on{false};  // the last lane-group solve ran the exact-size hipRTC kernel
     mutable std::atomic<bool> grp_ct_on{false};   // ... with the network compiled in (mk_group.h: ct_rhs)
     mutable std::atomic<bool> grp_quad_on{false}; // ... the quad-group kernel (mk_quad.h)
+    mutable std::atomic<int> grp_lanes{0};        // lanes per condition of the last lane-group solve
 };
 
 // FNV-1a 64 over the solver-side structure (network.py: structural_digest)
@@ -498,6 +499,12 @@ extern "C" int pck_network_dims(const pck_network* net, int32_t* dims) {
     return PCK_OK;
 }
 
+extern "C" int pck_network_group_lanes(const pck_network* net, int32_t* lanes) {
+    if (!net || !lanes) return fail(PCK_E_ARG, "null argument%s", "");
+    *lanes = net->grp_lanes.load(std::memory_order_relaxed);
+    return PCK_OK;
+}
+
 extern "C" int pck_network_set_plan_mode(pck_network* net, int mode) {
     if (!net) return fail(PCK_E_ARG, "null network%s", "");
     if (mode < PCK_PLAN_AUTO || mode > PCK_PLAN_GROUP) return fail(PCK_E_ARG, "unknown plan mode%s %lld", "", mode);
@@ -816,7 +823,7 @@ __global__ void __launch_bounds__(256) k_select_status(int64_t n, const int32_t*
 // column instead of its 4 corners (A/B: 2.57 ms; the longer preview costs
 // more than the extra samples find).
 constexpr int PCK_PREVIEW_LANES_MAX = 8;
-// the preview lanes, the wavefront sort, k_select_ordered and k_solve's
+// the preview lanes, the wavefront sort and k_solve's
 // worder mapping all take one block of the lane solver to be one wavefront
 static_assert(PCK_SOLVE_BLOCK == 64, "cost-ordered dispatch assumes one wavefront per lane-solver block");
 __device__ __forceinline__ int preview_lane(int k, int np) {
@@ -842,18 +849,23 @@ __global__ void __launch_bounds__(256) k_preview_list(int64_t n, int64_t W, int 
 // one-block sort below reads W contiguous keys (it read 4 W scattered lines
 // itself: ~28 of its 70 us)
 // st (screening previews): a sample whose screening trip is not accepted
-// counts `reject` more steps
+// counts `reject` more steps, and its wavefront's wrej flag is set (the
+// solve skips that wavefront's screening trip, mk_solver.h: k_solve)
 __global__ void __launch_bounds__(256) k_wave_keys(int64_t n, int64_t W, int np, const int32_t* ns,
-                                                   const int32_t* st, int reject, int32_t* wkey) {
+                                                   const int32_t* st, int reject, int32_t* wkey, int32_t* wrej) {
     const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (w >= W) return;
     int k = 0;
+    bool rej = false;
     for (int l = 0; l < np; ++l) {
         int64_t c = w * PCK_SOLVE_BLOCK + preview_lane(l, np);
         c = (c < n) ? c : n - 1;
-        k = max(k, ns[c] + ((st && st[c] != PCK_ST_OK) ? reject : 0));
+        const bool r = st && st[c] != PCK_ST_OK;
+        rej = rej || r;
+        k = max(k, ns[c] + (r ? reject : 0));
     }
     wkey[w] = min(max(k, 0), 1023);
+    wrej[w] = rej ? 1 : 0;
 }
 
 // descending counting sort of the wavefronts by their key (one block).
@@ -881,58 +893,6 @@ __global__ void __launch_bounds__(1024) k_wave_order(int64_t W, const int32_t* w
     for (int64_t w = tid; w < W; w += 1024) order[atomicAdd(&hist[wkey[w]], 1)] = (int32_t)w;
 }
 
-// The retry list of the wavefronts at positions [0, nw) of a dispatch order
-// (k_select_status restricted to them): one wave of threads per wavefront.
-__global__ void __launch_bounds__(256) k_select_ordered(int64_t n, const int32_t* wo, int64_t nw,
-                                                        const int32_t* status, int32_t want, int64_t* idx,
-                                                        int32_t* cnt) {
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t p = t >> 6;
-    const int lane = threadIdx.x & 63;
-    const int64_t c = (p < nw) ? (int64_t)wo[p] * PCK_SOLVE_BLOCK + lane : n;
-    const bool f = (c < n) && status[c] == want;
-    const unsigned long long m = __ballot(f);
-    if (m == 0ull) return;                             // wave-uniform
-    int base = 0;
-    if (lane == 0) base = atomicAdd(cnt, (int)__popcll(m));
-    base = __shfl(base, 0, 64);
-    if (f) idx[base + __popcll(m & ((1ull << lane) - 1ull))] = c;
-}
-
-// A second stream (and two events) per host thread and device, for the
-// degenerate-root retry of the first wavefronts of an ordered first pass to
-// run beside the rest of it; never destroyed (process lifetime).
-struct SideStream {
-    hipStream_t s = nullptr;
-    hipEvent_t first = nullptr, done = nullptr;
-};
-static int side_stream(SideStream** out) {
-    static thread_local SideStream ss[64];
-    int dev = 0;
-    HIPCHK(hipGetDevice(&dev));
-    if (dev < 0 || dev >= 64) return fail(PCK_E_HIP, "device index%s out of range", "");
-    SideStream& x = ss[dev];
-    if (!x.s) {
-        HIPCHK(hipStreamCreateWithFlags(&x.s, hipStreamNonBlocking));
-        HIPCHK(hipEventCreateWithFlags(&x.first, hipEventDisableTiming));
-        HIPCHK(hipEventCreateWithFlags(&x.done, hipEventDisableTiming));
-    }
-    *out = &x;
-    return PCK_OK;
-}
-
-// Fraction of the ordered wavefronts (the cheapest, dispatched last) whose
-// first pass runs beside the retry of the others (PCK_RETRY_OVERLAP, 0 = off).
-// Off by default: on the 1024^2 volcano the split costs more than it hides
-// (r3s A/B: 7.50 ms off; 8.14 / 8.07 / 8.36 / 8.99 ms at 0.2 / 0.3 / 0.45 / 0.6)
-// because the second half-launch starts with a cold tail of 1-step waves and
-// the retry waves then compete with it for the same CUs.
-static double retry_overlap() {
-    const char* e = getenv("PCK_RETRY_OVERLAP");
-    const double v = e ? atof(e) : 0.0;
-    return (v > 0.0 && v < 1.0) ? v : 0.0;
-}
-
 // One solver launch over the batch (lane or lane-group path).
 // lanes > 0 (lane path with an index list of known length): launch only that
 // many lanes instead of n * G
@@ -950,7 +910,8 @@ static int run_solver(const pck_network* net, const pck_conditions* cond, const 
         // solves of networks of at most 16 species: the quad-group kernel
         // (mk_quad.h), four lanes per condition (steady solves with its Newton
         // polish unless PCK_GRP_QUAD_NEWTON=0)
-        if (NS <= 16 && (!a.newton || grp_quad_newton_enabled()) && !a.cons_rows &&
+        // (an explicit screening pass runs on the 16-lane kernel, which has it)
+        if (NS <= 16 && (!a.newton || grp_quad_newton_enabled()) && !a.cons_rows && a.screen_rtol <= 0.0 &&
             net->plan_mode != PCK_PLAN_RUNTIME && jit_enabled() &&
             grp_quad_enabled(NS, net->nv.NRXN) && grp_ct_enabled(G, net->nv.NRXN) && !net->jit_grp_src.empty()) {
             hipFunction_t fq =
@@ -971,11 +932,13 @@ static int run_solver(const pck_network* net, const pck_conditions* cond, const 
                 net->grp_jit_on.store(true, std::memory_order_relaxed);
                 net->grp_ct_on.store(false, std::memory_order_relaxed);
                 net->grp_quad_on.store(true, std::memory_order_relaxed);
+                net->grp_lanes.store(4, std::memory_order_relaxed);
                 HIPCHK(hipGetLastError());
                 return PCK_OK;
             }
         }
         net->grp_quad_on.store(false, std::memory_order_relaxed);
+        net->grp_lanes.store(G, std::memory_order_relaxed);
         dim3 g((unsigned)((groups + per - 1) / per));
         hipFunction_t f = nullptr;
         int P = grp_p(NS);
@@ -1121,22 +1084,24 @@ static int launch_solve(const pck_network* net, const pck_conditions* cond, cons
         a.cons_rows = (e && e[0] == '1');
     }
     const bool grp = drc_groups || use_group(net, a.G);
-    // the screening pass inside the solve (the default: a lane or group that
-    // fails it solves again at once, so the slow second solves overlap the
-    // bulk of the first pass) or, for pck_solve on the one-lane path, as two
-    // launches (PCK_SCREEN_INLINE=0, A/B)
-    const bool screen_inline =
-        screen && (grp || drc_groups || a.G != 1 || !(getenv("PCK_SCREEN_INLINE") && getenv("PCK_SCREEN_INLINE")[0] == '0'));
+    // the screening pass inside the solve: a lane or group that fails it
+    // solves again at once, so the slow second solves overlap the bulk of the
+    // first pass (as two launches, the second latency-bound on its slowest
+    // solve, it was 3.26 against 2.93 ms per volcano step; DESIGN.md
+    // "Screening pass")
     {
         a.screen_max_steps = std::min(a.max_steps, 2000);
         const char* e = getenv("PCK_SCREEN_MAX_STEPS");
         if (e && atoi(e) > 0) a.screen_max_steps = std::min(a.max_steps, atoi(e));
     }
-    if (screen_inline) {
+    if (screen) {
+        // the 64-lane group kernel carries one integrator copy (mk_group.h:
+        // k_solve_grp): a screening request there is refused, not ignored
+        if (grp && grp_g(net->nv.NDYN) == 64)
+            return fail(PCK_E_ARG, "screen_rtol: no screening pass on networks of more than 32 dynamic species%s", "");
         a.screen_rtol = prm->screen_rtol;
         a.screen_atol = a.atol * (prm->screen_rtol / a.rtol);
         a.screen_dist = a.root_dist * (prm->screen_margin > 0.0 ? prm->screen_margin : 0.1);
-        screen = false;
     }
     if (grp && !net->grp_ok)
         return fail(PCK_E_SIZE, "lane-group solver: a reaction has more than 6 dynamic participants%s", "");
@@ -1169,7 +1134,7 @@ static int launch_solve(const pck_network* net, const pck_conditions* cond, cons
         // the preview runs the screening trip where the solve screens
         const bool pscreen = a.screen_rtol > 0.0 && !(getenv("PCK_PREVIEW_RULE") && getenv("PCK_PREVIEW_RULE")[0] == '0');
         const size_t b_list = sizeof(int64_t) * (size_t)W * np, b_ns = sizeof(int32_t) * (size_t)n;
-        rc = salloc(oscr, b_list + 64 + 2 * b_ns + 2 * sizeof(int32_t) * (size_t)W, s);
+        rc = salloc(oscr, b_list + 64 + 2 * b_ns + 3 * sizeof(int32_t) * (size_t)W, s);
         if (rc) return rc;
         int64_t* list = oscr.as<int64_t>();
         int32_t* cnt = (int32_t*)((char*)list + b_list);
@@ -1177,6 +1142,7 @@ static int launch_solve(const pck_network* net, const pck_conditions* cond, cons
         int32_t* pst = pns + n;                     // screening previews: the samples' statuses
         int32_t* wo = pst + n;
         int32_t* wkey = wo + W;                     // per-wavefront sort key, compact
+        int32_t* wrej = wkey + W;                   // per wavefront: a screening sample was not accepted
         hipLaunchKernelGGL(k_preview_list, dim3((unsigned)((W * np + 255) / 256)), dim3(256), 0, s,
                            n, W, np, list, cnt);
         HIPCHK(hipGetLastError());
@@ -1212,7 +1178,9 @@ static int launch_solve(const pck_network* net, const pck_conditions* cond, cons
             pv.newton = a.newton;
             pv.root_dist = a.screen_dist;
         }
-        pv.max_steps = a.max_steps < 1000 ? a.max_steps : 1000;
+        // the transient preview's cap; a screening preview runs the trip with
+        // the solve's own cap, so that its verdict is the trip's
+        pv.max_steps = pscreen ? a.screen_max_steps : (a.max_steps < 1000 ? a.max_steps : 1000);
         {
             // A/B: PCK_PREVIEW_MAXSTEPS, a lower cap (a capped sample counts as
             // rejected: its wavefront goes first and skips the screening trip)
@@ -1229,7 +1197,7 @@ static int launch_solve(const pck_network* net, const pck_conditions* cond, cons
             if (e) reject = atoi(e);
         }
         hipLaunchKernelGGL(k_wave_keys, dim3((unsigned)((W + 255) / 256)), dim3(256), 0, s, n, W, np, pns,
-                           pscreen ? pst : nullptr, reject, wkey);
+                           pscreen ? pst : nullptr, reject, wkey, wrej);
         HIPCHK(hipGetLastError());
         hipLaunchKernelGGL(k_wave_order, dim3(1), dim3(1024), 0, s, W, wkey, wo);
         HIPCHK(hipGetLastError());
@@ -1241,17 +1209,11 @@ static int launch_solve(const pck_network* net, const pck_conditions* cond, cons
         // full transient instead of the screening one: the same root to the
         // refinement's rounding (~1e-13).  PCK_SCREEN_SKIP=0 turns it off.
         if (pscreen && !(getenv("PCK_SCREEN_SKIP") && getenv("PCK_SCREEN_SKIP")[0] == '0')) {
-            a.wkey = wkey;
-            a.skip_key = reject;
+            a.wrej = wrej;
         }
-        // issue priority for the costliest wavefronts (PCK_PRIO_WAVES: a
-        // count, or a fraction of the launch's wavefronts below 1)
-        const char* e = getenv("PCK_PRIO_WAVES");
-        const double pw = e ? atof(e) : 0.0;
-        a.prio_waves = (int)(pw < 1.0 ? pw * (double)W : pw);
     }
     StreamScratch rscr;
-    if (retry || screen) {
+    if (retry) {
         // the retry list (int64 per condition), its length, and a status
         // array when the caller passed none
         // (W wavefronts' worth of entries: the overlapped split keeps two lists)
@@ -1261,78 +1223,7 @@ static int launch_solve(const pck_network* net, const pck_conditions* cond, cons
         if (rc) return rc;
         if (!a.status) a.status = (int32_t*)(rscr.as<char>() + sizeof(int64_t) * nl + 64);
     }
-    const double ovl = (retry && a.worder) ? retry_overlap() : 0.0;
-    if (ovl > 0.0) {
-        // ordered first pass in two launches: the first K wavefronts (the
-        // costliest), then the rest; the retry of the first K runs on a side
-        // stream beside the second launch, the retry of the rest after it
-        const int64_t W = (n + PCK_SOLVE_BLOCK - 1) / PCK_SOLVE_BLOCK;
-        int64_t K = W - (int64_t)(ovl * (double)W);
-        K = K < 1 ? 1 : (K > W - 1 ? W - 1 : K);
-        SideStream* ss = nullptr;
-        rc = side_stream(&ss);
-        if (rc) return rc;
-        int64_t* list1 = rscr.as<int64_t>();
-        int64_t* list2 = list1 + K * PCK_SOLVE_BLOCK;
-        int32_t* cnt = (int32_t*)(list1 + W * PCK_SOLVE_BLOCK);
-        HIPCHK(hipMemsetAsync(cnt, 0, 2 * sizeof(int32_t), s));
-        SolveArgs r = a;
-        r.rtol = prm->retry_rtol;
-        r.atol = prm->retry_atol;
-        r.newton = 0;
-        r.retry_pass = 1;
-        r.worder = nullptr;
-        const int32_t* wo = a.worder;
-        rc = run_solver(net, cond, a, grp, ga, traj, kf, kr, s, K * PCK_SOLVE_BLOCK);
-        if (rc) return rc;
-        HIPCHK(hipEventRecord(ss->first, s));
-        HIPCHK(hipStreamWaitEvent(ss->s, ss->first, 0));
-        hipLaunchKernelGGL(k_select_ordered, dim3((unsigned)((K * 64 + 255) / 256)), dim3(256), 0, ss->s, n, wo, K,
-                           a.status, (int32_t)PCK_ST_NEWTON, list1, cnt);
-        HIPCHK(hipGetLastError());
-        r.idx = list1;
-        r.nidx = cnt;
-        rc = run_solver(net, cond, r, grp, ga, traj, kf, kr, ss->s, K * PCK_SOLVE_BLOCK);
-        if (rc) return rc;
-        HIPCHK(hipEventRecord(ss->done, ss->s));
-        SolveArgs a2 = a;
-        a2.worder = wo + K;
-        rc = run_solver(net, cond, a2, grp, ga, traj, kf, kr, s, (W - K) * PCK_SOLVE_BLOCK);
-        if (rc) return rc;
-        hipLaunchKernelGGL(k_select_ordered, dim3((unsigned)(((W - K) * 64 + 255) / 256)), dim3(256), 0, s, n,
-                           wo + K, W - K, a.status, (int32_t)PCK_ST_NEWTON, list2, cnt + 1);
-        HIPCHK(hipGetLastError());
-        r.idx = list2;
-        r.nidx = cnt + 1;
-        rc = run_solver(net, cond, r, grp, ga, traj, kf, kr, s, (W - K) * PCK_SOLVE_BLOCK);
-        if (rc) return rc;
-        HIPCHK(hipStreamWaitEvent(s, ss->done, 0));        // the caller's stream sees both retries
-        retry = false;                                     // done
-    } else if (screen) {
-        // pass 1: the steady rule at screen_rtol (atol scaled alike), a root
-        // accepted only within screen_margin * root_dist of the transient end
-        SolveArgs a1 = a;
-        a1.rtol = prm->screen_rtol;
-        a1.atol = a.atol * (prm->screen_rtol / a.rtol);
-        a1.root_dist = a.root_dist * (prm->screen_margin > 0.0 ? prm->screen_margin : 0.1);
-        a1.max_steps = a.screen_max_steps;
-        rc = run_solver(net, cond, a1, grp, ga, traj, kf, kr, s);
-        if (rc) return rc;
-        // pass 2: every other condition, from y0 at the caller's tolerances
-        int64_t* idx = rscr.as<int64_t>();
-        int32_t* cnt = (int32_t*)(idx + ((n + PCK_SOLVE_BLOCK - 1) / PCK_SOLVE_BLOCK) * PCK_SOLVE_BLOCK);
-        HIPCHK(hipMemsetAsync(cnt, 0, sizeof(int32_t), s));
-        hipLaunchKernelGGL(k_select_status, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, a.status, -1,
-                           idx, cnt);
-        HIPCHK(hipGetLastError());
-        SolveArgs a2 = a;
-        a2.idx = idx;
-        a2.nidx = cnt;
-        a2.retry_pass = 2;
-        a2.worder = nullptr;
-        rc = run_solver(net, cond, a2, grp, ga, false, kf, kr, s);
-        if (rc) return rc;
-    } else {
+    {
         rc = run_solver(net, cond, a, grp, ga, traj, kf, kr, s);
         if (rc) return rc;
     }

@@ -22,11 +22,13 @@
 // (whole rows, LAPACK storage) and the solves apply the row permutation to
 // the right-hand side first.
 //
-// Scope: transient solves (newton = 0) without trajectories or conservation
-// rows -- the BASELINE CH4 (SteadyStateSolver transient to 1e4 s) and DMTM
-// DRC (2R+1 transients per condition) configurations.  Steady solves (the
-// Newton polish), trajectories and PCK_CONS_ROWS keep the lane-group kernel
-// (csrc/mk_kernels.hip: run_solver).
+// Scope: every group solve of a network of at most 16 dynamic species --
+// transients (the BASELINE CH4 SteadyStateSolver transient to 1e4 s, the
+// DMTM DRC's 2R+1 transients per condition), steady solves with the quad
+// Newton polish (q_newton) and trajectories (TRAJ, RODAS4P dense output);
+// each is its own instantiation k_solve_q4<Net, NEWTON, TRAJ>.  An explicit
+// screening pass (SolveArgs::screen_rtol) and PCK_CONS_ROWS run on the
+// 16-lane kernel instead (csrc/mk_kernels.hip: run_solver).
 #pragma once
 #include "mk_group.h"
 

@@ -191,20 +191,12 @@ struct Lane {
 //   f_i = rs_i * sum_j S_ij (kf_j prod c^a - kr_j prod c^b) + fl_i (in_i - y_i),
 //   c_i = cf_i y_i,  rs_i = rs0_i + rsT_i T.
 // ---------------------------------------------------------------------------
-// rf - rr as written (PCK_NET_EXACT=1): with FMA contraction the compiler may
-// fold the last product of rr into the subtraction, and the two rates then no
-// longer cancel exactly where they agree -- on the lane-group kernel that
-// noise turned some 1e12 s DMTM transients into 80x more steps
-// (mk_group.h: ct_sub)
-#ifndef PCK_NET_EXACT
-#define PCK_NET_EXACT 0
-#endif
-__device__ __forceinline__ double net_rate(double rf, double rr) {
-#if PCK_NET_EXACT
-#pragma clang fp contract(off)
-#endif
-    return rf - rr;
-}
+// rf - rr: the lane solver lets the compiler contract the last product of
+// rr into the subtraction (rounding it as written cost the volcano 4 % with
+// unchanged step counts, profiles/r4; the lane-group kernels round it as
+// written, mk_group.h: ct_sub, where the contraction noise cost DMTM
+// transients 80x more steps -- DESIGN.md)
+__device__ __forceinline__ double net_rate(double rf, double rr) { return rf - rr; }
 
 template <class P, class K>
 __device__ __forceinline__ void rhs(const P& p, const Lane<P::NS>& L, const K& k, const double (&y)[P::NS],
@@ -1253,15 +1245,11 @@ struct SolveArgs {
     // most max_steps): a trip past it is not accepted and the full solve runs
     // (an optimisation never costs more than this many steps per lane)
     int screen_max_steps;
-    // cost-ordered dispatch: the first prio_waves blocks of the order (the
-    // costliest wavefronts) raise their issue priority on the SIMD
-    int prio_waves;
-    // screening with a screening-rule preview: a wavefront whose key is at
-    // least skip_key (some preview sample was not accepted) runs the single
+    // screening with a screening-rule preview: a wavefront one of whose
+    // preview samples was not accepted (k_wave_keys: wrej) runs the single
     // pass directly (its screening trip would lengthen the wave's critical
-    // path for nothing); wkey == nullptr: never
-    const int32_t* wkey;
-    int skip_key;
+    // path for nothing); wrej == nullptr: never
+    const int32_t* wrej;
 };
 
 // One condition's solve: transient from y0, then (with a.newton) the Newton
@@ -1280,7 +1268,10 @@ __device__ __forceinline__ int solve_lane(const P& p, const Lane<P::NS>& L, cons
         for (int i = 0; i < NS; ++i) y[i] = cv.y0[i * cv.ld_y0 + c * cv.s_y0];
         st = integrate<TRAJ>(p, L, k, y, a.t0, a.t_end, a.screen_rtol, a.screen_atol, a.screen_max_steps, nsp,
                              a.cons_rows != 0, to);
-        if (st == PCK_ST_OK && a.newton) st = newton(p, L, k, y, a.newton_iters, a.screen_dist, a.screen_atol);
+        // the acceptance test's absolute term is the caller's atol, not the
+        // trip's scaled one (3e4 x larger): a trace species must be as close
+        // to its root as the single pass requires
+        if (st == PCK_ST_OK && a.newton) st = newton(p, L, k, y, a.newton_iters, a.screen_dist, a.atol);
         total = nsp;
         if (st == PCK_ST_OK) {
             ns = total;
@@ -1345,10 +1336,6 @@ __global__ void __launch_bounds__(PCK_SOLVE_BLOCK) __attribute__((amdgpu_waves_p
         __syncthreads();
     }
 #endif
-    // the costliest wavefronts of a cost-ordered launch take issue priority
-    // over the rest of the SIMD's waves, so that they progress at near their
-    // own latency while the cheap waves fill the issue slots they leave
-    if (a.worder && (int)blockIdx.x < a.prio_waves) __builtin_amdgcn_s_setprio(2);
 #if PCK_WAVE_TIMES
     const long long wt0 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -1382,7 +1369,7 @@ __global__ void __launch_bounds__(PCK_SOLVE_BLOCK) __attribute__((amdgpu_waves_p
         load_keff(p, nv, cv, c, kf, kr, ld_k, k, pj, pfac);
         double y[NS];
         TrajOut to{a.t_out, a.n_out, a.traj, a.ld_traj, c};
-        const bool screen_on = !(a.wkey && a.worder && a.wkey[a.worder[blockIdx.x]] >= a.skip_key);
+        const bool screen_on = !(a.wrej && a.worder && a.wrej[a.worder[blockIdx.x]]);
         st = solve_lane<TRAJ>(p, L, k, cv, c, a, y, ns, to, screen_on);
         tof = lane_tof(p, nv, k, y);
         bool fin = isfinite(tof);

@@ -42,7 +42,10 @@ class LinearForm:
         c = dict(self.clamps)
         c.update(other.clamps)
         r = dict(self.refs)
-        r.update(other.refs)
+        for name, st in other.refs.items():
+            if r.setdefault(name, st) is not st:
+                raise ValueError('energy terms of two different states named %r meet in one expression; '
+                                 'state names must be unique within a network' % name)
         return LinearForm(t, c, r)
 
     def __add__(self, o):

@@ -66,6 +66,13 @@ class DeviceNetwork:
         L.check(self.lib.pck_network_dims(self.h, dims))
         return int(dims[10])
 
+    def group_lanes(self):
+        """Lanes per condition of the last lane-group solve: 4 (quad-group
+        kernel), 16, 32 or 64 (group width G); 0 before any group solve."""
+        g = C.c_int32(0)
+        L.check(self.lib.pck_network_group_lanes(self.h, C.byref(g)))
+        return int(g.value)
+
     def set_plan_mode(self, mode):
         """A/B switch: 0 / False = auto, 1 / True = runtime plan (never the
         compiled-in one), 2 = lane-group solver."""

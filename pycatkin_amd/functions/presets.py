@@ -8,16 +8,24 @@ Outputs (CSV names and columns) follow the reference.
 from __future__ import annotations
 
 import os
+import warnings
 
 import numpy as np
 
 from ..constants.physical_constants import bartoPa
 
 
+def _no_plots(what, *flags):
+    """Plotting is out of scope: every driver warns and skips it,
+    so a reference script that asks for figures still gets its numbers."""
+    if any(flags):
+        warnings.warn('%s: plotting is not part of pycatkin_amd; the figures are skipped '
+                      '(use save_results for the CSVs)' % what, stacklevel=3)
+
+
 def run(sim_system, steady_state_solve=False, plot_results=False, save_results=False, fig_path=None, csv_path=''):
-    """presets.py:16-28 (plotting is out of scope: plot_results raises)."""
-    if plot_results:
-        raise NotImplementedError('plotting (System.plot_transient) is not part of pycatkin_amd')
+    """presets.py:16-28 (plotting is out of scope: plot_results warns and is skipped)."""
+    _no_plots('run', plot_results)
     sim_system.solve_odes()
     if save_results:
         sim_system.write_results(path=csv_path)
@@ -73,6 +81,7 @@ def run_temperatures(sim_system, temperatures, steady_state_solve=False, tof_ter
                      fig_path=None, csv_path=''):
     """presets.py:31-167 as one batch over `temperatures`.  Returns
     (final [nT, n_states], rates [nT, n_reactions], drcs {T: {reaction: xi}})."""
+    _no_plots('run_temperatures', plot_results, plot_transient)
     temps = np.asarray(temperatures, float).ravel()
     plan = sim_system.plan()
     r = sim_system.solve_batch(T=temps, steady=steady_state_solve)
@@ -101,8 +110,7 @@ def run_parameters(sim_system, parameters, params_name, steady_state_solve=False
     value, one launch each.  As in the reference, sim_system.params keeps the
     last value afterwards."""
     vals = np.asarray(parameters, float).ravel()
-    if plot_results or plot_transient:
-        raise NotImplementedError('plotting is out of scope (DESIGN.md); use save_results')
+    _no_plots('run_parameters', plot_results, plot_transient)
     batched = (params_name in ('temperature', 'pressure') or params_name.startswith('start_state_')
                or params_name.startswith('inflow_state_'))
     if batched:

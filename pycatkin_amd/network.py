@@ -334,7 +334,11 @@ def energy_program(forms, states, descriptors=None):
     th_dbl = np.zeros((NTH, 5))
     freqs = []
     for s_i, sname in enumerate(th_found):
-        st = states[sname] if (states and sname in states) else refs[sname]
+        # the State object the form was built from: a reaction-derived
+        # reaction's energies come from its base system's states
+        # (reaction.py:312-339), which may share names with this system's own
+        # (Butadiene: the DFT base's 'H2' vs the MKM's mass-only 'H2')
+        st = refs[sname] if sname in refs else states[sname]
         kind = 0
         uf = np.zeros(0)
         if st.Gvibr is None:

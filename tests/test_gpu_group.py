@@ -415,6 +415,17 @@ def test_synthetic_fixture_parity(P, synthetic):
         assert 0.5 * ROOT_DIST <= fx['crit'][f] <= 2.0 * ROOT_DIST, info['flips']
 
 
+def test_screening_refused_on_64_lane_groups(P, synthetic):
+    """The 64-lane group kernel carries one integrator copy and no screening
+    trip: an explicit screen on the 50-species network is refused (C-ABI
+    PCK_E_ARG), not silently run as a single pass."""
+    sim, _ = synthetic
+    D = np.zeros((2, 4))
+    with pytest.raises(RuntimeError, match='screen'):
+        sim.solve_batch(T=np.full(2, 500.0), desc={'D%d' % k: D[:, k] for k in range(4)}, steady=True,
+                        screen=3e-2, max_steps=50)
+
+
 def test_group_exact_size_kernel_matches_compiled(P, inputs, monkeypatch):
     """The lane-group solver hipRTC specialises for the network's exact size
     (k_solve_grp<11, 16, 1> for DMTM) and the compiled-in padded kernel
@@ -724,15 +735,19 @@ def test_group_screening_pass_matches_single_pass(P, inputs, monkeypatch):
     is not accepted (group-uniform) -- report what the single pass reports:
     the same statuses, the same roots to the refinement's rounding, the same
     transient ends bitwise (mk_group.h: k_solve_grp).  The quad kernel,
-    which runs these steady solves by default, does not screen (a single
-    pass), so the 16-lane kernel is pinned here (PCK_GRP_QUAD_NEWTON=0)."""
+    which runs the plain steady solves of this network by default, has no
+    screening trip: an explicit screen runs on the 16-lane kernel
+    (pck_network_group_lanes reports 16), and the single pass is pinned to
+    that kernel too (PCK_GRP_QUAD_NEWTON=0) for the bitwise comparison."""
     from pycatkin_amd.classes.system import SCREEN_RTOL
-    monkeypatch.setenv('PCK_GRP_QUAD_NEWTON', '0')
     s = _dmtm(P, inputs)
     TT, pp = np.meshgrid(np.linspace(450.0, 750.0, 8), np.logspace(4.0, 6.0, 8), indexing='ij')
     kw = dict(T=TT.ravel(), p=pp.ravel(), steady=True)
-    a = s.solve_batch(screen=None, **kw)
     b = s.solve_batch(screen=SCREEN_RTOL, **kw)
+    assert s.device().group_lanes() == 16
+    monkeypatch.setenv('PCK_GRP_QUAD_NEWTON', '0')
+    a = s.solve_batch(screen=None, **kw)
+    monkeypatch.delenv('PCK_GRP_QUAD_NEWTON')
     assert np.array_equal(a['status'], b['status']), (a['status'], b['status'])
     ok = a['status'] == 0
     assert ok.mean() > 0.5

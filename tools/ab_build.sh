@@ -4,7 +4,7 @@
 # -> pycatkin_amd/_ab/lib_<name>.so ; run one with PCK_LIB=<path> python bench.py ...
 # Variants build one after the other, each with the product's parallel split
 # build (__graft_entry__.compile_library); diagnostic builds whose __device__
-# counters the C-ABI reads back (-DPCK_PHASE, -DPCK_TRACE) are one
+# counters the C-ABI reads back (-DPCK_PHASE, -DPCK_TRACE, -DPCK_WAVE_TIMES) are one
 # translation unit, as the counters must live in the unit that reads them.
 set -e
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
@@ -14,7 +14,7 @@ mkdir -p "$ROOT/pycatkin_amd/_ab"
 while [ $# -ge 2 ]; do
   name=$1; flags=$2; shift 2
   case "$flags" in
-    *PCK_PHASE*|*PCK_TRACE*)
+    *PCK_PHASE*|*PCK_TRACE*|*PCK_WAVE_TIMES*)
       /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fno-signed-zeros -mllvm -amdgpu-sched-strategy=max-ilp \
           -shared -fPIC $flags -I"$ROOT/include" -o "$ROOT/pycatkin_amd/_ab/lib_$name.so" \
           "$ROOT/pycatkin_amd/csrc/mk_kernels.hip" -lhiprtc ;;
