@@ -1582,10 +1582,17 @@ __device__ __forceinline__ int grp_newton(const NetView& nv, const GrpView& gv, 
     bool conv = false;
     double prev = INFINITY, lastq = 1.0;
     int linear = 0;
+    bool pv = false;
+#pragma unroll
+    for (int l = 0; l < PCK_MAX_CONS; ++l) pv = pv || (l < nv.NCONS && x.gl == piv_l[l]);
+    // mk_solver.h: newton_pinned -- a species at exactly 0 with an exactly
+    // zero rate at the transient end is held at 0 (its Newton steps dropped)
+    bool pin = false;
     for (int it = 0; it < iters; ++it) {
         double Gv;
         // the rounding floor (mk_solver.h: PCK_BALANCE_CONV)
         const double bal = grp_imbalance<NSP, G, Net>(nv, gv, x, z, Gv);
+        if (it == 0) pin = x.row && !pv && z == 0.0 && Gv == 0.0;
         if (it >= 2 && bal_prev <= PCK_BALANCE_CONV && bal > bal_prev) { z = z_prev; conv = true; break; }
         bal_prev = bal;
         z_prev = z;
@@ -1611,6 +1618,7 @@ __device__ __forceinline__ int grp_newton(const NetView& nv, const GrpView& gv, 
         Gv = -Gv * scl;
         if (!grp_lu<NSP, G>(x, F)) break;
         double dz = grp_solve<NSP, G>(x, F, Gv);
+        if (pin) dz = 0.0;
         double alpha = 1.0;
         if (linear >= 2 && lastq < 0.9) {
             alpha = fmin(4.0, 1.0 / (1.0 - lastq));
@@ -1657,7 +1665,7 @@ __device__ __forceinline__ int grp_newton(const NetView& nv, const GrpView& gv, 
             }
             nprev = nr;
             if (r == PCK_NEWTON_REFINE || nr == 0.0) break;
-            const double dz = grp_solve<NSP, G>(x, F, Gv);
+            const double dz = pin ? 0.0 : grp_solve<NSP, G>(x, F, Gv);
             const double zmax = gmax<G>(x.row ? fabs(z) : 0.0);
             const double rel = gmax<G>(x.row ? fabs(dz) / fmax(fabs(z), 1e-12 * zmax + 1e-300) : 0.0);
             zp = z;

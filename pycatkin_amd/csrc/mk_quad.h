@@ -788,11 +788,12 @@ template <class Net>
 __device__ __forceinline__ int q_newton(const Quad& x, double (&y)[4], int iters, double dist, double atol) {
     constexpr int NS = Net::NS, NC = Net::NCONS;
     const int gl = x.gl;
-    bool real[4], pv[4];
+    bool real[4], pv[4], pin[4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
         real[s] = (4 * gl + s) < NS;
         pv[s] = false;
+        pin[s] = false;
     }
     // conservation laws: the lane's coefficients, totals at the transient end,
     // the pivot rows (compile-time rows, the lane that holds them at run time)
@@ -831,6 +832,11 @@ __device__ __forceinline__ int q_newton(const Quad& x, double (&y)[4], int iters
     for (int it = 0; it < iters; ++it) {
         double Gv[4];
         const double bal = imbalance(z, Gv);
+        if (it == 0) {
+            // mk_solver.h: newton_pinned -- zero species with a zero rate stay 0
+#pragma unroll
+            for (int s = 0; s < 4; ++s) pin[s] = real[s] && !pv[s] && z[s] == 0.0 && Gv[s] == 0.0;
+        }
         if (it >= 2 && bal_prev <= PCK_BALANCE_CONV && bal > bal_prev) {
 #pragma unroll
             for (int s = 0; s < 4; ++s) z[s] = zp[s];
@@ -886,7 +892,7 @@ __device__ __forceinline__ int q_newton(const Quad& x, double (&y)[4], int iters
         double zmax = 0.0;
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-            Gv[s] *= alpha;
+            Gv[s] = pin[s] ? 0.0 : Gv[s] * alpha;
             z[s] += Gv[s];
             if (real[s]) {
                 fin = fin && isfinite(z[s]);
@@ -957,6 +963,7 @@ __device__ __forceinline__ int q_newton(const Quad& x, double (&y)[4], int iters
             bool fin = true;
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
+                if (pin[s]) Gv[s] = 0.0;
                 if (real[s]) rl = fmax(rl, fabs(Gv[s]) / fmax(fabs(z[s]), 1e-12 * zmax + 1e-300));
                 zq[s] = z[s];
                 z[s] += Gv[s];

@@ -922,12 +922,32 @@ __device__ PCK_LANE_INLINE int newton(const P& p, const Lane<P::NS>& L, const K&
     bool conv = false;
     double prev = INFINITY, lastq = 1.0;
     int linear = 0;
+    // newton_pinned: a species at exactly 0 whose rate is exactly 0 at the
+    // transient end is held at 0 (its Newton steps are dropped here; the
+    // group kernels give it a unit row and a zero residual).  Such a species
+    // has no reaction that can produce it from the start state (every
+    // producer involves another such species or a zero inflow / pressure):
+    // the transient keeps it at 0 exactly, and the steady state on that
+    // invariant subspace has it at 0.  Left free, its Jacobian row (tiny after
+    // equilibration) loses the threshold pivot to a dense row, the LU's
+    // rounding lands on it, and the balance test then fails on a 1e-33
+    // residue (Butadiene with_jonas_byproducts: C4H9O2_2*, C4H8O2_3*, whose
+    // only source is ethyl acetate at zero pressure; oracle: _set_reach).
+    unsigned pinm = 0u;
     for (int it = 0; it < iters; ++it) {
         double G[NS], J[NS][NS];
         int piv[NS];
         {
             double Gg[NS];
             rhs_gross(p, L, k, z, G, Gg);
+            if (it == 0) {
+#pragma unroll
+                for (int i = 0; i < NS; ++i) {
+                    bool cp = false;
+                    for (int l = 0; l < p.ncons(); ++l) cp = cp || (p.cpiv(l) == i);
+                    if (!cp && z[i] == 0.0 && G[i] == 0.0) pinm |= 1u << i;
+                }
+            }
             const double bal = imbalance(p, G, Gg);
             if (it >= 2 && bal_prev <= PCK_BALANCE_CONV && bal > bal_prev) {   // the rounding floor
 #pragma unroll
@@ -982,7 +1002,7 @@ __device__ PCK_LANE_INLINE int newton(const P& p, const Lane<P::NS>& L, const K&
         bool finite = true;
 #pragma unroll
         for (int i = 0; i < NS; ++i) {
-            G[i] *= alpha;
+            G[i] = (pinm & (1u << i)) ? 0.0 : G[i] * alpha;
             z[i] += G[i];
             finite = finite && isfinite(z[i]);
             zmax = fmax(zmax, fabs(z[i]));
@@ -1107,8 +1127,9 @@ __device__ PCK_LANE_INLINE int newton(const P& p, const Lane<P::NS>& L, const K&
 #pragma unroll
             for (int i = 0; i < NS; ++i) {
                 z_prev[i] = z[i];
-                rel = fmax(rel, fabs(G[i]) / fmax(fabs(z[i]), 1e-12 * zmax + 1e-300));
-                z[i] += G[i];
+                const double d = (pinm & (1u << i)) ? 0.0 : G[i];
+                rel = fmax(rel, fabs(d) / fmax(fabs(z[i]), 1e-12 * zmax + 1e-300));
+                z[i] += d;
                 fin = fin && isfinite(z[i]);
             }
             // a refinement moves a converged root by rounding, not by 1e-6:
