@@ -1164,22 +1164,26 @@ static int launch_solve(const pck_network* net, const pck_conditions* cond, cons
             if (e) pv.atol = fmax(pv.atol, atof(e) * pv.rtol);
         }
         pv.newton = 0;
-        if (pscreen) {                               // the screening trip, as the solve runs it
-            pv.rtol = a.screen_rtol;
-            pv.atol = a.screen_atol;
+        if (pscreen) {
+            // the screening trip at a coarser rtol (0.1, atol scaled alike):
+            // its verdict orders the wavefronts and flags those that skip
+            // the trip; a cheaper preview that flags a few more of them
+            // measured 2.43 / 2.46 -> 2.38 / 2.38 ms per volcano step (rtol
+            // 0.05: 2.45, 0.15: 2.38, 0.2: 2.39; profiles/r6/ab_preview_screen_rtol.txt).
+            // PCK_PREVIEW_SCREEN_RTOL overrides it (A/B).
+            double prt = 0.1;
             {
-                // A/B: PCK_PREVIEW_SCREEN_RTOL, a coarser preview of the trip
                 const char* e = getenv("PCK_PREVIEW_SCREEN_RTOL");
-                if (e && atof(e) > a.screen_rtol) {
-                    pv.atol = a.screen_atol * (atof(e) / a.screen_rtol);
-                    pv.rtol = atof(e);
-                }
+                if (e && atof(e) > 0.0) prt = atof(e);
             }
+            prt = fmax(prt, a.screen_rtol);
+            pv.rtol = prt;
+            pv.atol = a.screen_atol * (prt / a.screen_rtol);
             pv.newton = a.newton;
             pv.root_dist = a.screen_dist;
         }
-        // the transient preview's cap; a screening preview runs the trip with
-        // the solve's own cap, so that its verdict is the trip's
+        // the transient preview's cap; a screening preview runs its trip with
+        // the solve's own trip cap
         pv.max_steps = pscreen ? a.screen_max_steps : (a.max_steps < 1000 ? a.max_steps : 1000);
         {
             // A/B: PCK_PREVIEW_MAXSTEPS, a lower cap (a capped sample counts as

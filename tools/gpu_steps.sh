@@ -12,12 +12,12 @@
 #   smoke              __graft_entry__.smoke()               -> OUT/smoke.log
 #   bench:ARGS         python bench.py ARGS (',' = ' ')      -> OUT/bench_<n>.json / .err
 #   benchlong:ARGS     the same with a 1000 s limit (synthetic 1e6)
-#   abbench:NAME:ARGS  bench.py ARGS on the A/B build pycatkin_amd/_ab/lib_NAME.so
+#   abbench:NAME:ARGS  bench.py ARGS on the A/B build pycatkin_amd/_abt/lib_NAME.so
 #   envbench:V=X:ARGS  bench.py ARGS with the environment variable V=X
 #   abenv:NAME:V=X:ARGS  abbench with the environment variable V=X
 #   py:SCRIPT,ARGS     python SCRIPT ARGS                    -> OUT/py_<n>.log
 #   profile:NAME:ARGS  tools/profile.sh OUT/NAME python3 bench.py ARGS
-#   ab:NAME,NAME...    tools/ab_run.sh variants (pycatkin_amd/_ab/lib_NAME.so)
+#   ab:NAME,NAME...    tools/ab_run.sh variants (pycatkin_amd/_abt/lib_NAME.so)
 set -u
 OUT=$1
 shift
@@ -40,10 +40,10 @@ for step in "$@"; do
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/$OUT/smoke.log 2>&1 ;;
     bench)
       timeout -k 10 400 python -u bench.py ${arg//,/ } > gpurun_out/$OUT/bench_$k.json 2> gpurun_out/$OUT/bench_$k.err ;;
-    abbench)            # abbench:NAME:ARGS -- bench.py ARGS on pycatkin_amd/_ab/lib_NAME.so
+    abbench)            # abbench:NAME:ARGS -- bench.py ARGS on pycatkin_amd/_abt/lib_NAME.so
       name=${arg%%:*}
       bargs=${arg#*:}
-      PCK_LIB=$PWD/pycatkin_amd/_ab/lib_$name.so timeout -k 10 400 python -u bench.py ${bargs//,/ } \
+      PCK_LIB=$PWD/pycatkin_amd/_abt/lib_$name.so timeout -k 10 400 python -u bench.py ${bargs//,/ } \
           > gpurun_out/$OUT/bench_$k.json 2> gpurun_out/$OUT/bench_$k.err ;;
     envbench)           # envbench:VAR=VALUE:ARGS -- bench.py ARGS with one environment variable set
       kv=${arg%%:*}
@@ -55,10 +55,13 @@ for step in "$@"; do
       rest=${arg#*:}
       kv=${rest%%:*}
       bargs=${rest#*:}
-      env "$kv" PCK_LIB=$PWD/pycatkin_amd/_ab/lib_$name.so timeout -k 10 400 python -u bench.py ${bargs//,/ } \
+      env "$kv" PCK_LIB=$PWD/pycatkin_amd/_abt/lib_$name.so timeout -k 10 400 python -u bench.py ${bargs//,/ } \
           > gpurun_out/$OUT/bench_$k.json 2> gpurun_out/$OUT/bench_$k.err ;;
     benchlong)
       timeout -k 10 1000 python -u bench.py ${arg//,/ } > gpurun_out/$OUT/bench_$k.json 2> gpurun_out/$OUT/bench_$k.err ;;
+    pyin)              # pyin:DIR:ARGS -- python ARGS run inside DIR
+      d=${arg%%:*}; pargs=${arg#*:}
+      (cd $d && timeout -k 10 400 python -u ${pargs//,/ }) > gpurun_out/$OUT/py_$k.log 2>&1 ;;
     py)
       timeout -k 10 400 python -u ${arg//,/ } > gpurun_out/$OUT/py_$k.log 2>&1 ;;
     profile)
