@@ -644,13 +644,8 @@ static bool use_group(const pck_network* net, int lanes_per_cond) {
 static inline int grp_g(int NS) { return NS <= 16 ? 16 : NS <= 32 ? 32 : 64; }
 // Jacobian column passes: the whole NS x NS block in LDS (one pass, 20 KiB
 // at NS = 50) -- measured 2.3x faster per Jacobian than 4 passes over a
-// 6 KiB block at NS = 50 (tools/phase_group.py).  PCK_GRP_PASSES=n forces
-// n passes (A/B).
-static inline int grp_p(int NS) {
-    const char* e = getenv("PCK_GRP_PASSES");
-    const int p = e ? atoi(e) : 1;
-    return (p >= 1 && p <= NS) ? p : 1;
-}
+// 6 KiB block at NS = 50 (tools/phase_group.py).
+static inline int grp_p(int) { return 1; }
 #define PCK_GRP_SWITCH(NS, CALL)              \
     if ((NS) <= 16) { CALL(16, 16, 1); }       \
     else if ((NS) <= 32) { CALL(32, 32, 1); }  \
@@ -815,20 +810,18 @@ __global__ void __launch_bounds__(256) k_select_status(int64_t n, const int32_t*
 // trips plus the full solves of the lanes the screening does not accept, so
 // the preview runs the screening trip itself (transient, Newton, the rule at
 // the screening distance) and a sample it does not accept adds
-// PCK_PREVIEW_REJECT (400) steps to the key.  With the transient-only
-// preview, wavefronts whose screening rejected lanes started mid-launch and
-// ended the launch 0.5 ms after the rest (tools/wave_timeline.py,
-// profiles/r5/wave_timeline_*): 2.71 -> 2.52 ms per 2^20 volcano step.
-// PCK_PREVIEW_LANES=8 samples rows 0, 5, 10, 15 x the patch's first and last
-// column instead of its 4 corners (A/B: 2.57 ms; the longer preview costs
-// more than the extra samples find).
-constexpr int PCK_PREVIEW_LANES_MAX = 8;
+// PCK_PREVIEW_REJECT_STEPS (400; 200 / 800 within noise) steps to the key.
+// With the transient-only preview, wavefronts whose screening rejected lanes
+// started mid-launch and ended the launch 0.5 ms after the rest
+// (tools/wave_timeline.py, profiles/r5/wave_timeline_*): 2.71 -> 2.52 ms per
+// 2^20 volcano step.  (8 samples per wavefront instead of its 4 corners:
+// 2.57 ms, the longer preview costs more than the extra samples find.)
+constexpr int PCK_PREVIEW_REJECT_STEPS = 400;
 // the preview lanes, the wavefront sort and k_solve's
 // worder mapping all take one block of the lane solver to be one wavefront
 static_assert(PCK_SOLVE_BLOCK == 64, "cost-ordered dispatch assumes one wavefront per lane-solver block");
-__device__ __forceinline__ int preview_lane(int k, int np) {
-    if (np == 4) return (k < 2) ? 3 * k : 60 + 3 * (k - 2);      // 0, 3, 60, 63
-    return 20 * (k >> 1) + 3 * (k & 1);                            // 0, 3, 20, 23, 40, 43, 60, 63
+__device__ __forceinline__ int preview_lane(int k, int) {
+    return (k < 2) ? 3 * k : 60 + 3 * (k - 2);                     // 0, 3, 60, 63
 }
 
 __global__ void __launch_bounds__(256) k_preview_list(int64_t n, int64_t W, int np, int64_t* list, int32_t* cnt) {
@@ -952,17 +945,9 @@ static int run_solver(const pck_network* net, const pck_conditions* cond, const 
             ct = f != nullptr;
         }
         if (!ct && (net->plan_mode != PCK_PLAN_RUNTIME || traj) && jit_enabled()) {
+            // (row loops bounded by the largest row degree measured slower:
+            // CH4 100.6 k -> 83.6 k solves/s, profiles/r2/configs/ab_degmax.txt)
             f = jit_group_kernel(NS, G, P, traj, false, net->grp_npmax, net->grp_emax, 0, bal);
-            // uniform row loops bounded by the largest row degree (PCK_GRP_DEGMAX):
-            // an A/B option (PCK_GRP_DEGMAX=1), taken only where they keep the
-            // occupancy; measured slower (CH4 100.6 k -> 83.6 k solves/s, DMTM
-            // DRC 68.5 k -> 67.3 k; profiles/r2/configs/ab_degmax.txt)
-            const char* ev = getenv("PCK_GRP_DEGMAX");
-            hipFunction_t fd = (f && ev && ev[0] == '1')
-                                   ? jit_group_kernel(NS, G, P, traj, false, net->grp_npmax, net->grp_emax,
-                                                      net->grp_degmax, bal)
-                                   : nullptr;
-            if (fd && grp_waves(fd) >= grp_waves(f)) { f = fd; degmax = net->grp_degmax; }
         }
         if (traj && !f) return fail(PCK_E_HIP, "hipRTC compile of the trajectory kernel failed%s", "");
         size_t shm;
@@ -1126,13 +1111,9 @@ static int launch_solve(const pck_network* net, const pck_conditions* cond, cons
                        (prm->wave_order > 0 || (prm->wave_order == 0 && n >= 262144));
     if (order) {
         const int64_t W = (n + PCK_SOLVE_BLOCK - 1) / PCK_SOLVE_BLOCK;
-        int np = 4;
-        {
-            const char* e = getenv("PCK_PREVIEW_LANES");
-            if (e && atoi(e) == PCK_PREVIEW_LANES_MAX) np = PCK_PREVIEW_LANES_MAX;
-        }
+        const int np = 4;
         // the preview runs the screening trip where the solve screens
-        const bool pscreen = a.screen_rtol > 0.0 && !(getenv("PCK_PREVIEW_RULE") && getenv("PCK_PREVIEW_RULE")[0] == '0');
+        const bool pscreen = a.screen_rtol > 0.0;
         const size_t b_list = sizeof(int64_t) * (size_t)W * np, b_ns = sizeof(int32_t) * (size_t)n;
         rc = salloc(oscr, b_list + 64 + 2 * b_ns + 3 * sizeof(int32_t) * (size_t)W, s);
         if (rc) return rc;
@@ -1158,11 +1139,6 @@ static int launch_solve(const pck_network* net, const pck_conditions* cond, cons
             if (e) pv.rtol = fmax(a.rtol, atof(e));
         }
         pv.atol = a.atol * (pv.rtol / a.rtol);       // the same atol / rtol ratio
-        {
-            // A/B: PCK_PREVIEW_ATOL = a floor of the preview's atol, relative to its rtol
-            const char* e = getenv("PCK_PREVIEW_ATOL");
-            if (e) pv.atol = fmax(pv.atol, atof(e) * pv.rtol);
-        }
         pv.newton = 0;
         if (pscreen) {
             // the screening trip at a coarser rtol (0.1, atol scaled alike):
@@ -1184,24 +1160,14 @@ static int launch_solve(const pck_network* net, const pck_conditions* cond, cons
         }
         // the transient preview's cap; a screening preview runs its trip with
         // the solve's own trip cap
+        // (lower caps, 30 / 50 steps, flagged most wavefronts: 2.9x the steps)
         pv.max_steps = pscreen ? a.screen_max_steps : (a.max_steps < 1000 ? a.max_steps : 1000);
-        {
-            // A/B: PCK_PREVIEW_MAXSTEPS, a lower cap (a capped sample counts as
-            // rejected: its wavefront goes first and skips the screening trip)
-            const char* e = getenv("PCK_PREVIEW_MAXSTEPS");
-            if (e && atoi(e) > 0) pv.max_steps = std::min(pv.max_steps, atoi(e));
-        }
         pv.y = nullptr; pv.tof = nullptr; pv.status = pscreen ? pst : nullptr; pv.nsteps = pns;
         pv.idx = list; pv.nidx = cnt; pv.retry_pass = 0; pv.worder = nullptr;
         rc = run_solver(net, cond, pv, grp, ga, traj, kf, kr, s, W * np);
         if (rc) return rc;
-        int reject = 400;
-        {
-            const char* e = getenv("PCK_PREVIEW_REJECT");
-            if (e) reject = atoi(e);
-        }
         hipLaunchKernelGGL(k_wave_keys, dim3((unsigned)((W + 255) / 256)), dim3(256), 0, s, n, W, np, pns,
-                           pscreen ? pst : nullptr, reject, wkey, wrej);
+                           pscreen ? pst : nullptr, PCK_PREVIEW_REJECT_STEPS, wkey, wrej);
         HIPCHK(hipGetLastError());
         hipLaunchKernelGGL(k_wave_order, dim3(1), dim3(1024), 0, s, W, wkey, wo);
         HIPCHK(hipGetLastError());
@@ -1211,10 +1177,8 @@ static int launch_solve(const pck_network* net, const pck_conditions* cond, cons
         // screening trip only delays it): 2.53 -> 2.40 ms per 2^20 volcano
         // step.  Their accepted lanes then report the root reached from the
         // full transient instead of the screening one: the same root to the
-        // refinement's rounding (~1e-13).  PCK_SCREEN_SKIP=0 turns it off.
-        if (pscreen && !(getenv("PCK_SCREEN_SKIP") && getenv("PCK_SCREEN_SKIP")[0] == '0')) {
-            a.wrej = wrej;
-        }
+        // refinement's rounding (~1e-13).
+        if (pscreen) a.wrej = wrej;
     }
     StreamScratch rscr;
     if (retry) {
