@@ -335,7 +335,8 @@ def _solve_workload(wl, sim, net, plan, n, T, p, desc, tof_terms, steady, activi
     scr = ((SCREEN_RTOL if net.NDYN <= SCREEN_MAX_LANE_SPECIES else 0.0)
            if getattr(args, 'screen', None) is None else args.screen)
     if steady and wl.prm.newton and wl.prm.root_dist > 0.0 and not args.retry and scr > 0.0:
-        wl.prm.screen_rtol, wl.prm.screen_margin = float(scr), SCREEN_MARGIN
+        wl.prm.screen_rtol = float(scr)
+        wl.prm.screen_margin = SCREEN_MARGIN if getattr(args, 'screen_margin', None) is None else args.screen_margin
     wl.tolerances = (wl.prm.rtol, wl.prm.atol)
     wl.prm.wave_order = {'auto': 0, 'on': 1, 'off': -1}[getattr(args, 'wave_order', 'auto')]
     # solver launches per step: the first pass, the degenerate-root retry and,
@@ -584,6 +585,8 @@ def build_parser():
     ap.add_argument('--atol', type=float, default=0.0, help='A/B: first-pass atol (0: the input\'s)')
     ap.add_argument('--retry', type=float, nargs=2, default=None, metavar=('RTOL', 'ATOL'),
                     help='A/B: integrate the status-4 conditions again at these tolerances (default: no retry)')
+    ap.add_argument('--screen-margin', type=float, default=None,
+                    help='screening acceptance as a fraction of the root distance (default SCREEN_MARGIN; A/B)')
     ap.add_argument('--screen', type=float, default=None,
                     help='screening-pass rtol of steady solves (default SCREEN_RTOL; 0: off)')
     ap.add_argument('--root-dist', type=float, default=None,
