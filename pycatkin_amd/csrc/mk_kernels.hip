@@ -1141,13 +1141,15 @@ static int launch_solve(const pck_network* net, const pck_conditions* cond, cons
         pv.atol = a.atol * (pv.rtol / a.rtol);       // the same atol / rtol ratio
         pv.newton = 0;
         if (pscreen) {
-            // the screening trip at a coarser rtol (0.1, atol scaled alike):
+            // the screening trip at a coarser rtol (0.2, atol scaled alike):
             // its verdict orders the wavefronts and flags those that skip
             // the trip; a cheaper preview that flags a few more of them
-            // measured 2.43 / 2.46 -> 2.38 / 2.38 ms per volcano step (rtol
-            // 0.05: 2.45, 0.15: 2.38, 0.2: 2.39; profiles/r6/ab_preview_screen_rtol.txt).
+            // measured 2.43 / 2.46 -> 2.38 / 2.38 ms per volcano step at 0.1,
+            // and 2.28 / 2.25 -> 2.23 / 2.22 ms at 0.2 with the screening
+            // margin 0.5 (0.05: 2.24 / 2.25, 0.3: 2.26;
+            // profiles/r6/ab_preview_screen_rtol.txt).
             // PCK_PREVIEW_SCREEN_RTOL overrides it (A/B).
-            double prt = 0.1;
+            double prt = 0.2;
             {
                 const char* e = getenv("PCK_PREVIEW_SCREEN_RTOL");
                 if (e && atof(e) > 0.0) prt = atof(e);
