@@ -341,7 +341,7 @@ def _solve_workload(wl, sim, net, plan, n, T, p, desc, tof_terms, steady, activi
     wl.prm.wave_order = {'auto': 0, 'on': 1, 'off': -1}[getattr(args, 'wave_order', 'auto')]
     # solver launches per step: the first pass, the degenerate-root retry and,
     # on the lane solver with cost-ordered dispatch, its preview
-    ordered = net.NDYN <= 8 and (wl.prm.wave_order == 1 or (wl.prm.wave_order == 0 and n >= 262144))
+    ordered = net.NDYN <= 8 and (wl.prm.wave_order == 1 or (wl.prm.wave_order == 0 and n >= 131072))
     # (the screening pass runs inside the first pass's launch)
     wl.solver_launches = 1 + int(bool(wl.prm.newton and wl.prm.retry_rtol > 0.0)) + int(ordered)
     wl.out, wl.o = _outputs(torch, net, n, L, _ptr)

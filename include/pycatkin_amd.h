@@ -152,10 +152,14 @@ typedef struct {
                             *   status stays PCK_ST_NEWTON and nsteps adds the retry's steps; a
                             *   retry that fails keeps the first pass's y / tof (PCK_ST_NEWTON_LOOSE) */
     int32_t wave_order;    /* pck_solve on the lane solver: dispatch the 64-condition wavefronts in
-                            *   descending cost, predicted by a loose preview transient (rtol 1e-3) of 4
-                            *   lanes of each; 1 on, -1 off, 0 auto (on for n >= 262144: more than one
-                            *   round of wavefronts).  Results do not depend on it: the same 64
-                            *   conditions share a wavefront either way. */
+                            *   descending cost, predicted by a preview of 4 lanes of each (a loose
+                            *   transient, or the screening trip at rtol 0.2 when the solve screens:
+                            *   a wavefront with a sample it does not accept skips its trip);
+                            *   1 on, -1 off, 0 auto (on for n >= 131072).  It pays where costs vary
+                            *   across the batch and is overhead on a uniform-cost sweep.  Results
+                            *   do not depend on it beyond rounding: the same 64 conditions share a
+                            *   wavefront either way, and a skipped trip's lanes answer from the
+                            *   full solve (the same root to ~1e-13). */
     double root_dist;      /* with newton (> 0): the Newton root is reported (PCK_ST_OK) only if the
                             *   transient end it started from lies within root_dist * |root_i| + atol
                             *   of it in every dynamic species -- the transient has reached that steady

@@ -462,7 +462,8 @@ class System:
 
     def solve_batch(self, T=None, p=None, desc=None, y0=None, fix=None, inflow=None, tof_terms=(),
                     steady=False, activity=False, t_end=None, t0=None, rtol=None, atol=None, max_steps=200000,
-                    newton_iters=60, to_numpy=True, t_out=None, retry=None, root_dist='auto', screen='auto'):
+                    newton_iters=60, to_numpy=True, t_out=None, retry=None, root_dist='auto', screen='auto',
+                    wave_order='auto'):
         """Transient solve to t_end (solve_odes), optionally polished to the
         steady state (find_steady), with TOF or activity per condition; with
         t_out, also the dynamic state at those times ('traj' [n_out, NS, n],
@@ -484,7 +485,14 @@ class System:
         not accept at the transient tolerances ('auto' on one-lane networks
         only; a number screens the 16- / 32-lane group networks too, a network
         of at most 16 species then running on the 16-lane kernel instead of
-        the quad one; networks of more than 32 species refuse it)."""
+        the quad one; networks of more than 32 species refuse it).
+        `wave_order` ('auto', 'on', 'off'; pck_solve_params.wave_order): the
+        one-lane solver's cost-ordered dispatch, a preview of 4 samples per
+        wavefront that puts the costliest wavefronts first ('auto': from
+        131 072 conditions).  It pays where costs vary a lot across the batch
+        (the volcano grid) and is overhead where they do not: a 262 144-
+        temperature CSTR sweep takes 1.71 ms with it off against 2.36 ms
+        (DESIGN.md "Round 6")."""
         plan = self.plan(tuple(tof_terms), None)
         net = self.device(tuple(tof_terms), None)
         sizes = [T, p] + (list(desc.values()) if desc else [])
@@ -513,7 +521,8 @@ class System:
                         max_steps=max_steps, newton=steady, newton_iters=newton_iters, activity=activity,
                         t_out=t_out, retry=_retry_tolerances(retry) if steady else None,
                         root_dist=float(root_dist) if steady else 0.0,
-                        screen=(float(screen), SCREEN_MARGIN) if (steady and screen) else None)
+                        screen=(float(screen), SCREEN_MARGIN) if (steady and screen) else None,
+                        wave_order={'auto': 0, 'on': 1, 'off': -1}[wave_order])
         if to_numpy:
             return {k: v.cpu().numpy() for k, v in out.items()}
         return out
