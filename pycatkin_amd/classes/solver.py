@@ -79,6 +79,33 @@ class SteadyStateSolver:
                   % (not rate_fail, not ssum_fail, not negjac_fail, surf_sum, rate_residual, float(np.max(eig.real))))
         return not any([rate_fail, spos_fail, ssum_fail, negjac_fail])
 
+    def test_convergence_batch(self, Y, desc=None, T=None, rate_tol=1e-4, coverage_tol=5e-2, pos_jac_tol=1e-2,
+                               log=False, **kwargs):
+        """test_convergence for surface states Y [n_surface, n] (index_map
+        order) in two launches (rates, Jacobians), each column at its own
+        temperature / descriptor energies; the eigenvalues of the n Jacobians
+        in one batched LAPACK call."""
+        Y = np.asarray(Y, float)
+        n = Y.shape[1]
+        if n == 0:
+            return np.zeros(0, bool)
+        f = self.sys._fun_ss_batch(Y, desc=desc, T=T)
+        J = self.sys._jac_ss_batch(Y, desc=desc, T=T)
+        rate_fail = np.max(np.abs(f), axis=0) > rate_tol
+        spos_fail = np.any(np.round(Y, 2) < 0, axis=0)
+        y_all = np.concatenate((np.repeat(self.ygas[:, None], n, axis=1), Y))
+        surf_sum = np.array([y_all[sorted(idx)].sum(axis=0) for idx in self.sys.coverage_map.values()])
+        ssum_fail = np.any(np.abs(surf_sum - 1) > coverage_tol, axis=0)
+        eig = np.linalg.eigvals(np.moveaxis(J, 2, 0))
+        negjac_fail = np.any(eig.real > pos_jac_tol, axis=1)
+        if log:
+            for c in range(n):
+                print('    - CHECKS: rate %s | surf_sum %s | jac_eigV %s\n        - surf_sum = %s\n'
+                      '        - rate_residual = %s\n        - jacobian_eigV_max = %s'
+                      % (not rate_fail[c], not ssum_fail[c], not negjac_fail[c], [float(v) for v in surf_sum[:, c]],
+                         float(np.max(np.abs(f[:, c]))), float(np.max(eig[c].real))))
+        return ~(rate_fail | spos_fail | ssum_fail | negjac_fail)
+
     def _norm(self, y_surf):
         """solver.py:122-141"""
         y_surf = np.where(np.asarray(y_surf, float) < self.sys.min_tol, self.sys.min_tol, y_surf).astype(float)
@@ -138,14 +165,7 @@ class SteadyStateSolver:
         r = s.solve_batch(T=T, y0=np.repeat(y0[:, None], T.size, axis=1), t0=0.0, t_end=tmax, rtol=1e-10,
                           atol=1e-12, steady=False, max_steps=max_steps)
         Y = r['y'][s._from_plan(plan)]
-        ok = np.zeros(T.size, bool)
-        T_keep = s.T
-        try:
-            for c in range(T.size):
-                s.T = float(T[c])
-                ok[c] = (r['status'][c] == 0) and self.test_convergence(Y[:, c], **kw)
-        finally:
-            s.T = T_keep
+        ok = (r['status'] == 0) & self.test_convergence_batch(Y, T=T, **kw)
         return Y, ok
 
     def _newton(self, x0, max_iters):

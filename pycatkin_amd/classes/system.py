@@ -123,6 +123,15 @@ class System:
                            atol=atol, xtol=xtol, ftol=ftol, jacobian=use_jacobian, nsteps=int(nsteps),
                            ode_solver=ode_solver, verbose=verbose)
 
+    def __deepcopy__(self, memo):
+        """A deep copy (butadiene_mkm.py:47, analysis.py:40) starts with an
+        empty plan cache: device networks are not copied."""
+        out = self.__class__.__new__(self.__class__)
+        memo[id(self)] = out
+        for k, v in self.__dict__.items():
+            setattr(out, k, {} if k == '_plans' else copy.deepcopy(v, memo))
+        return out
+
     # patched-API attribute names
     @property
     def T(self):
@@ -241,18 +250,20 @@ class System:
         fx = np.array([y_full[idx[s]] for s in plan.fix]) * float(self.p)
         return yd, fx
 
-    def _rates_batch(self, Y):
+    def _rates_batch(self, Y, desc=None):
         """forward / backward rates [n_reactions, m] (rate_map order) at full
-        compositions Y [n_species, m] (gas fractions x p), one device launch."""
+        compositions Y [n_species, m] (gas fractions x p), one device launch;
+        `desc` {name: [m]} for a network with descriptor energies."""
         plan, net, ngas = self._patched_eval()
         Y = np.asarray(Y, float)
         m = Y.shape[1]
         idx = self.index_map
         yd = Y[[idx[s] for s in plan.dyn]]
         fx = Y[[idx[s] for s in plan.fix]] * float(self.p)
-        T, p = float(self.T), float(self.p)
-        kf, kr = net.rate_constants(m, np.full(m, T), p)
-        rf, rr = net.reaction_rates(m, np.full(m, T), p, yd, kf, kr, None, fx)
+        T, p, d, _, _, _ = self._inputs(net, plan, m, np.full(m, float(self.T)), float(self.p), desc,
+                                        None, None, None)
+        kf, kr = net.rate_constants(m, T, p, d)
+        rf, rr = net.reaction_rates(m, T, p, yd, kf, kr, d, fx)
         rf, rr = rf.cpu().numpy(), rr.cpu().numpy()
         names = list(self.rate_map)
         order = [plan.reactions.index(name) for name in names]
@@ -268,6 +279,11 @@ class System:
         """system.py:396-416: reaction_matrix @ (r_fwd - r_rev) for every tracked species."""
         rates = self._calc_rates(y)
         return self.reaction_matrix @ (rates[:, 0] - rates[:, 1])
+
+    def get_dydt_batch(self, Y, desc=None):
+        """get_dydt for compositions Y [n_species, m] in one launch."""
+        rf, rr = self._rates_batch(Y, desc)
+        return self.reaction_matrix @ (rf - rr)
 
     def get_forward_only(self, y):
         """system.py:418-433 (the reference multiplies by the backward column)."""
@@ -320,18 +336,21 @@ class System:
         """system.py:547-564: surface block of the Jacobian (device pck_jacobian)."""
         return self._jac_ss_batch(np.asarray(y_surf, float)[:, None])[:, :, 0]
 
-    def _fun_ss_batch(self, Y):
-        """_fun_ss for a batch of surface states Y [n_surface, n] in one launch."""
+    def _fun_ss_batch(self, Y, desc=None, T=None):
+        """_fun_ss for a batch of surface states Y [n_surface, n] in one launch
+        (`desc` / `T`: per-condition descriptor energies / temperatures)."""
         plan, net, ngas = self._patched_eval()
         n = Y.shape[1]
-        T, p, d, fx, y0, inflow = self._inputs(net, plan, n, float(self.T), None, None, None, None, None)
+        T = float(self.T) if T is None else T
+        T, p, d, fx, y0, inflow = self._inputs(net, plan, n, T, None, desc, None, None, None)
         kf, kr = net.rate_constants(n, T, p, d)
         return net.species_rates(n, T, p, self._to_plan(plan, Y), kf, kr, d, fx, inflow).cpu().numpy()[self._from_plan(plan)]
 
-    def _jac_ss_batch(self, Y):
+    def _jac_ss_batch(self, Y, desc=None, T=None):
         plan, net, ngas = self._patched_eval()
         n = Y.shape[1]
-        T, p, d, fx, y0, inflow = self._inputs(net, plan, n, float(self.T), None, None, None, None, None)
+        T = float(self.T) if T is None else T
+        T, p, d, fx, y0, inflow = self._inputs(net, plan, n, T, None, desc, None, None, None)
         kf, kr = net.rate_constants(n, T, p, d)
         J = net.jacobian(n, T, p, self._to_plan(plan, Y), kf, kr, d, fx, inflow).cpu().numpy()
         inv = self._from_plan(plan)
