@@ -372,8 +372,9 @@ def volcano_workload(args, rank, world):
     set_volcano_energies(sim)
     plan = sim.plan(('CO_ox',))
     net = sim.device(('CO_ox',))
-    net.set_plan_mode(1 if args.runtime_plan else 0)
-    wl.kernel_name = 'k_solve<PlanRT<4>>' if (args.runtime_plan or not net.compiled_plan) else 'k_solve<PlanCT<Volcano>>'
+    net.set_plan_mode(2 if args.group else 1 if args.runtime_plan else 0)
+    wl.kernel_name = ('k_solve_grp<4, 16>' if args.group else 'k_solve<PlanRT<4>>'
+                      if (args.runtime_plan or not net.compiled_plan) else 'k_solve<PlanCT<Volcano>>')
     G = args.grid
     if args.scaling == 'strong':
         if G % world:
@@ -601,7 +602,7 @@ def build_parser():
     ap.add_argument('--runtime-plan', action='store_true',
                     help='A/B: force the runtime-plan solver instead of the compiled-in network')
     ap.add_argument('--group', action='store_true',
-                    help='A/B (cstr): one 16-lane group per condition (the lane-group solver) instead of one lane')
+                    help='A/B (cstr, volcano): one 16-lane group per condition (the lane-group solver) instead of one lane')
     ap.add_argument('--device', choices=('gpu', 'cpu-standin'), default='gpu', help=argparse.SUPPRESS)
     return ap
 
