@@ -730,6 +730,10 @@ def main(argv=None):
         if not cpu:
             fps = flops_per_step(wl.plan)
             fl_struct = fps * steps_local
+            # a group network of at most 16 species ran on the quad kernel
+            # unless it was kept on the 16-lane one (pck_network_group_lanes)
+            if wl.kernel_name == 'k_solve_grp<16, 16>' and wl.net.group_lanes() == 4:
+                wl.kernel_name = 'k_solve_q4<Jit>'
             pmc, traffic_src = profiled_counters(wl.kernel_name, wl.tag)
             # launches of the solver kernel per step (first pass, retry over the
             # compacted list, cost-order preview): the profile's per-launch
