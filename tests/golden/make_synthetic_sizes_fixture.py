@@ -1,7 +1,8 @@
-"""Oracle fixture of two smaller synthetic networks (pycatkin_amd/functions/
+"""Oracle fixture of three smaller synthetic networks (pycatkin_amd/functions/
 synthetic.py: synthetic_network(n_species, n_reactions, seed=1)), one per
-group kernel below the 64-lane one:
+group kernel:
 
+  syn40   40 dynamic species / 120 reactions -> the 64-lane group kernel
   syn24   24 dynamic species / 72 reactions  -> the 32-lane group kernel
   syn12   12 dynamic species / 36 reactions  -> the quad-group kernel
 
@@ -28,7 +29,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 OUT = os.path.join(HERE, 'synthetic_sizes_fixture.npz')
-NETS = {'syn24': (24, 72), 'syn12': (12, 36)}
+NETS = {'syn40': (40, 120), 'syn24': (24, 72), 'syn12': (12, 36)}
 SEED_NET = 1
 N = 64
 T = 500.0

@@ -1,6 +1,7 @@
-"""Random stiff networks on the 32-lane and quad-group kernels: the synthetic
-generator (pycatkin_amd/functions/synthetic.py, the BASELINE configs[4]
-family) at 24 species / 72 reactions and 12 species / 36 reactions, 64
+"""Random stiff networks on every group kernel: the synthetic generator
+(pycatkin_amd/functions/synthetic.py, the BASELINE configs[4] family) at 40
+species / 120 reactions (64-lane kernel, its Newton polish included), 24 /
+72 (32-lane) and 12 / 36 (quad), 64
 random-descriptor conditions each, steady-state rule to t_end = 1e8 s,
 against tests/golden/synthetic_sizes_fixture.npz (make_synthetic_sizes_fixture.py:
 the oracle's steady rule, lsoda at rtol 1e-11 / atol 1e-20).
@@ -50,8 +51,9 @@ def test_synthetic_sizes_fixture_reproduces(fx, key):
     plan = sim.plan(('R0',))
     assert sorted(plan.dyn) == sorted(str(x) for x in fx[key + '_dyn'])
     assert len(plan.dyn) == NETS[key][0]
-    assert fx[key + '_ok'].all()
-    for k in (0, 5):
+    # (syn40: the oracle's transient exceeds its budget at 2 of 64 conditions)
+    assert fx[key + '_ok'].sum() >= 62
+    for k in [k for k in range(8) if fx[key + '_ok'][k]][:2]:
         m = O.ClassicModel(spec_of(net, fx['desc'][k], float(T)), T=float(T))
         r = O.steady_rule(m, dist=ROOT_DIST, dist_atol=STEADY_ATOL, budget=400000, t_end=T_END)
         assert bool(r['regular']) == bool(fx[key + '_regular'][k])
@@ -69,7 +71,7 @@ def P():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('key,lanes', [('syn24', 32), ('syn12', 4)])
+@pytest.mark.parametrize('key,lanes', [('syn40', 64), ('syn24', 32), ('syn12', 4)])
 def test_synthetic_sizes_steady_vs_oracle(P, fx, key, lanes):
     """One steady solve of the 64 conditions (System.solve_batch(steady=True),
     the default STEADY_TRANSIENT tolerances) on the kernel the network's size
@@ -87,14 +89,15 @@ def test_synthetic_sizes_steady_vs_oracle(P, fx, key, lanes):
     assert set(np.unique(st).tolist()) <= {0, 4}, np.unique(st, return_counts=True)
     names = [str(x) for x in fx[key + '_dyn']]
     y = r['y'][[plan.dyn.index(nm) for nm in names]].T
+    ok = fx[key + '_ok']                    # conditions the oracle answered
     reg, dev = fx[key + '_regular'], st == 0
-    flips = np.nonzero(dev != reg)[0]
+    flips = np.nonzero((dev != reg) & ok)[0]
     for f in flips:
         assert 0.5 * ROOT_DIST <= fx[key + '_crit'][f] <= 2.0 * ROOT_DIST, (key, int(f), st[f], fx[key + '_crit'][f])
     assert len(flips) <= 2, flips
     ref = fx[key + '_y']
-    both = dev & reg
-    neither = ~dev & ~reg
+    both = dev & reg & ok
+    neither = ~dev & ~reg & ok
     assert both.sum() >= 50, both.sum()
     err = np.abs(y - ref) / (np.abs(ref) + 1e-300)
     ok_root = np.abs(y - ref) <= 1e-6 * np.abs(ref) + 1e-20
