@@ -110,3 +110,29 @@ def test_synthetic_sizes_steady_vs_oracle(P, fx, key, lanes):
     # the site balance holds on every condition
     C = plan.conservation
     np.testing.assert_allclose(C @ r['y'], np.repeat((C @ plan.y0_default)[:, None], n, axis=1), rtol=0, atol=1e-10)
+
+
+@pytest.mark.gpu
+def test_synthetic_drc_on_32_lane_groups(P, fx):
+    """The steady degree of rate control (old_system.py:490-515,
+    System.drc_batch(steady=True): 2 R + 1 = 145 group solves per condition)
+    of the 24-species network at two conditions, against
+    tests/golden/synthetic_drc_fixture.npz (make_synthetic_drc_fixture.py: the
+    oracle's steady rule for every perturbed system) at 1e-6 on every xi;
+    the sum rule (sum_j xi_j = 1) holds to 1e-6."""
+    from pycatkin_amd.functions.synthetic import synthetic_system
+    dfx = dict(np.load(os.path.join(HERE, 'golden', 'synthetic_drc_fixture.npz')))
+    assert dfx['all_regular'].all()
+    sim, _ = synthetic_system(_net('syn24'), t_end=T_END)
+    plan = sim.plan(('R0',))
+    rows = dfx['rows']
+    D = fx['desc'][rows]
+    out = sim.drc_batch(('R0',), T=np.full(rows.size, float(T)), desc={'D%d' % k: D[:, k] for k in range(4)},
+                        eps=float(dfx['eps']), steady=True)
+    assert sim.device(('R0',)).group_lanes() == 32
+    assert np.all(out['status'] == 0), out['status']
+    np.testing.assert_allclose(out['tof0'], dfx['tof0'], rtol=1e-6)
+    xi = np.array([out['R%d' % j] for j in range(len(plan.reactions))]).T
+    err = np.abs(xi - dfx['xi'])
+    assert err.max() <= 1e-6, (err.max(), np.unravel_index(np.argmax(err), err.shape))
+    np.testing.assert_allclose(xi.sum(axis=1), 1.0, atol=1e-6)
