@@ -136,3 +136,28 @@ def test_synthetic_drc_on_32_lane_groups(P, fx):
     err = np.abs(xi - dfx['xi'])
     assert err.max() <= 1e-6, (err.max(), np.unravel_index(np.argmax(err), err.shape))
     np.testing.assert_allclose(xi.sum(axis=1), 1.0, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_synthetic_trajectory_on_32_lane_groups(P, fx):
+    """Trajectory samples (solve_batch(t_out=...), the RODAS4P dense output
+    of the 32-lane kernel) of the 24-species network at four conditions, 31
+    log-spaced samples 0 .. 1e4 s at rtol 1e-10 / atol 1e-14, against
+    tests/golden/synthetic_traj_fixture.npz (the oracle's model, LSODA at
+    1e-12 / 1e-20 with t_eval; BDF agrees to 2.5e-8) at 1e-6 relative with
+    a 1e-12 floor."""
+    from pycatkin_amd.functions.synthetic import synthetic_system
+    tfx = dict(np.load(os.path.join(HERE, 'golden', 'synthetic_traj_fixture.npz')))
+    sim, _ = synthetic_system(_net('syn24'))
+    plan = sim.plan()
+    rows = tfx['rows']
+    D = fx['desc'][rows]
+    r = sim.solve_batch(T=np.full(rows.size, float(T)), desc={'D%d' % k: D[:, k] for k in range(4)}, t0=0.0,
+                        t_end=float(tfx['t_out'][-1]), rtol=1e-10, atol=1e-14, t_out=tfx['t_out'])
+    assert sim.device().group_lanes() == 32
+    assert np.all(r['status'] == 0), r['status']
+    pos = [plan.dyn.index(str(nm)) for nm in tfx['dyn']]
+    traj = r['traj'][:, pos, :]                          # [n_out, NS, n]
+    ref = np.transpose(tfx['traj'], (1, 2, 0))           # [n_out, NS, n]
+    bad = ~(np.abs(traj - ref) <= 1e-6 * np.abs(ref) + 1e-12)
+    assert not bad.any(), (np.argwhere(bad)[:6].tolist(), np.abs(traj - ref).max())
